@@ -1,0 +1,257 @@
+/*
+ * youth_icp.h — C-ABI of the MI355X-native RGBD frame-to-frame ICP path.
+ *
+ * This library drops in behind the reference's AlgorithmModule slot
+ * (SeunghwanByun/SLAM-RGBD, Youth.Source/AlgorithmModule/).  Two groups of
+ * entry points:
+ *
+ *   1. The reference's own C API, same names / argument meaning / return
+ *      convention, so existing callers link unchanged:
+ *        - SLAM.h:11-38        initSlamModule .. resetSlam
+ *        - algorithmModule.h:6 algorithmModule (pthread start routine)
+ *      Return convention (SLAM.h:21,26,30; SLAM.cpp:127-129,178-181):
+ *      int 1 = success, 0 = failure / not running.  Nothing throws across
+ *      this boundary; errors are logged to stderr.
+ *
+ *   2. An additive batch / device API (build-only; SURVEY §8b last row) used
+ *      by the multi-pair configs and the benchmark.  These return
+ *      YOUTH_OK (0) or a negative YOUTH_E* code.
+ *
+ * Plain C99: no torch types, no HIP types (streams travel as void*).
+ * Caller-owned host buffers are borrowed for the duration of the call only
+ * (SLAM.cpp:133-148 copies before returning); the library owns all device
+ * memory it allocates.
+ */
+#ifndef YOUTH_ICP_H
+#define YOUTH_ICP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------ */
+/* Types                                                                     */
+/* ------------------------------------------------------------------------ */
+
+/* Pinhole intrinsics + depth scale.  Defaults follow
+ * AlgorithmModule/config/astra_orb_slam3_rgbd.yaml:9-12,35 (fx=fy=570.3,
+ * cx=320, cy=240, DepthMapFactor=1000) and, for any W x H, the viewer's
+ * convention viewerModule.c:343-345 (f = 570.3, c = (W/2, H/2) integer). */
+typedef struct youth_intrinsics {
+    float fx, fy, cx, cy;
+    float depth_scale; /* depth units per metre (1000 = millimetres) */
+} youth_intrinsics;
+
+/* ICP parameters (this build's spec; the reference has no ICP). */
+typedef struct youth_icp_params {
+    int   iters;        /* fixed Gauss-Newton iterations, no early exit */
+    float dist_thresh;  /* correspondence gate |P' - P_t| < dist_thresh (m) */
+} youth_icp_params;
+
+/* Per-pair status bits returned by the batch API. */
+#define YOUTH_STATUS_OK          0
+#define YOUTH_STATUS_DEGENERATE  1 /* an iteration's 6x6 system was singular: update skipped */
+#define YOUTH_STATUS_FEW_MATCHES 2 /* an iteration had < 6 correspondences: update skipped */
+
+/* Return codes of the additive API. */
+#define YOUTH_OK        0
+#define YOUTH_EINVAL   -1 /* bad argument */
+#define YOUTH_ENOMEM   -2 /* device / host allocation failed */
+#define YOUTH_EHIP     -3 /* a HIP runtime call failed (see youth_icp_last_error) */
+#define YOUTH_ENODEV   -4 /* no HIP device visible */
+
+/* Number of fp64 values in one normal-equation record:
+ * [0..20] upper triangle of J^T J (row-major, i<=j), [21..26] J^T r,
+ * [27] sum r^2, [28] correspondence count. */
+#define YOUTH_NEQ 29
+
+typedef struct youth_icp_ctx youth_icp_ctx;
+
+/* ------------------------------------------------------------------------ */
+/* 1. Reference API (drop-in)                                                */
+/* ------------------------------------------------------------------------ */
+
+/* Replaces SLAM.h:11 / SLAM.cpp:67-95.  Parses Camera.fx/fy/cx/cy/width/height
+ * and DepthMapFactor from the YAML at config_file (NULL or unreadable file:
+ * viewer defaults).  vocabulary_file is accepted and ignored (no ORB
+ * vocabulary in an ICP tracker).  Starts the private worker thread. */
+void initSlamModule(const char* config_file, const char* vocabulary_file);
+
+/* Replaces SLAM.h:14 / SLAM.cpp:97-124: stop the worker, drop the queue. */
+void stopSlamModule(void);
+
+/* Replaces SLAM.h:22 / SLAM.cpp:126-175.  Copies depth (int16 mm, 0 =
+ * invalid) into the bounded ingest queue (size > 10 -> drop oldest down to 5,
+ * SLAM.cpp:163-168) and returns 1; 0 when not running or on bad arguments.
+ * color_data may be NULL (ICP does not use colour). */
+int processSlamFrame(const int16_t* depth_data, const uint8_t* color_data,
+                     int width, int height, uint32_t timestamp);
+
+/* Replaces SLAM.h:27 / SLAM.cpp:177-198: writes "<map_file>_trajectory.txt"
+ * (TUM: ts tx ty tz qx qy qz qw).  ts is the caller's timestamp in ms
+ * printed as-is (the reference passes ms as "seconds", SLAM.cpp:151). */
+int saveSlamMap(const char* map_file);
+
+/* Replaces SLAM.h:31. */
+int isSlamModuleRunning(void);
+
+/* Replaces SLAM.h:35: number of valid 3-D points in the latest tracked frame. */
+int getSlamMapPoints(void);
+
+/* Replaces SLAM.h:38: clear the trajectory and the reference frame. */
+void resetSlam(void);
+
+/* Replaces algorithmModule.h:6 (algorithmModule.c:3-5 calls an undefined
+ * SLAM()).  pthread start routine: starts the module if it is not running
+ * (arg, if non-NULL, is a const char* config path), then blocks until
+ * stopSlamModule() and returns NULL. */
+void* algorithmModule(void* id);
+
+/* ------------------------------------------------------------------------ */
+/* 2. Additive API                                                           */
+/* ------------------------------------------------------------------------ */
+
+/* Viewer-convention intrinsics for W x H (f = 570.3, c = (W/2, H/2)). */
+youth_intrinsics youth_default_intrinsics(int width, int height);
+youth_icp_params youth_default_params(void);
+
+/* Human-readable text of the last error on this thread ("" if none). */
+const char* youth_icp_last_error(void);
+
+/* Number of visible HIP devices (0 when none; never fails). */
+int youth_icp_device_count(void);
+
+/* One-shot host API:  aligns n_pairs independent pairs; src and
+ * dst are [n_pairs][H][W] int16 host arrays.  T_out: [n_pairs][16] row-major
+ * fp32 4x4 with P_dst = T * P_src.  assoc_out: nullable [n_pairs][H*W] int32
+ * final-iteration correspondence index (v'*W+u') or -1.  Uses device 0 and a
+ * cached context. */
+int youth_icp_align_batch(const int16_t* src, const int16_t* dst, int n_pairs,
+                          int W, int H, const youth_intrinsics* K, int iters,
+                          float* T_out, int32_t* assoc_out);
+
+/* Context: device workspace sized for max_frames frames of W x H.  The pair
+ * batch API uses 2 frames per pair; the sequence API one per frame. */
+youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
+                                const youth_intrinsics* K,
+                                const youth_icp_params* P);
+void youth_icp_destroy(youth_icp_ctx* ctx);
+
+/* Device-resident align of n_pairs pairs.  d_src / d_dst: device pointers to
+ * [n_pairs][H][W] int16.  T_init: nullable HOST [n_pairs][16] fp64 (identity
+ * if NULL).  d_T_out: nullable DEVICE [n_pairs][16] fp32.  stream: a
+ * hipStream_t as void* (NULL = the context's own stream).  Asynchronous:
+ * returns after enqueueing; use youth_icp_sync / youth_icp_get_poses. */
+int youth_icp_align_pairs_device(youth_icp_ctx* ctx, const int16_t* d_src,
+                                 const int16_t* d_dst, int n_pairs,
+                                 const double* T_init, float* d_T_out,
+                                 void* stream);
+
+/* Streamed-sequence align (config C5): d_frames [n_frames][H][W] int16 on
+ * device; computes the n_frames-1 relative poses T_k (P_k = T_k P_{k+1});
+ * every frame is back-projected and normal-estimated once. */
+int youth_icp_align_sequence_device(youth_icp_ctx* ctx, const int16_t* d_frames,
+                                    int n_frames, float* d_T_out, void* stream);
+
+/* Block until the context's last enqueued work on `stream` is done. */
+int youth_icp_sync(youth_icp_ctx* ctx, void* stream);
+
+/* Copy results of the last align to host (synchronises).  T64: [n][16] fp64
+ * (nullable), T32: [n][16] fp32 (nullable), status: [n] int32 (nullable). */
+int youth_icp_get_poses(youth_icp_ctx* ctx, int n, double* T64, float* T32,
+                        int32_t* status);
+
+/* Per-iteration diagnostics of the last align: [n][iters] correspondence
+ * counts and sums of squared residuals (nullable). */
+int youth_icp_get_stats(youth_icp_ctx* ctx, int n, int iters, double* count,
+                        double* sum_r2);
+
+/* Kernel timing (HIP events on the launch stream around every normal-equation
+ * reduction launch; for bench.py's roofline).  enable=1 resets counters. */
+int youth_icp_set_timing(youth_icp_ctx* ctx, int enable);
+/* total_ms / launches of reduction (kind 0), solve (1), frame-prep (2). */
+int youth_icp_get_timing(youth_icp_ctx* ctx, int kind, double* total_ms,
+                         int* launches);
+
+/* --- Stage-level entry points (validation / parity tests) --------------- */
+
+/* Depth -> XYZ planes (+ normals when want_normals) for n_frames host frames.
+ * Outputs are HOST arrays [n_frames][H*W] each (any may be NULL).  Same
+ * kernel as the align path. */
+int youth_icp_prepare_host(youth_icp_ctx* ctx, const int16_t* depth,
+                           int n_frames, int want_normals, float* X, float* Y,
+                           float* Z, float* NX, float* NY, float* NZ);
+
+/* One association + reduction pass for one pair at a GIVEN fp32 pose
+ * T12 (3x4 row-major).  src/dst host depth frames.  assoc: nullable
+ * [H*W] int32; neq: nullable [YOUTH_NEQ] fp64. */
+int youth_icp_reduce_host(youth_icp_ctx* ctx, const int16_t* src,
+                          const int16_t* dst, const float* T12, int32_t* assoc,
+                          double* neq);
+
+/* Solve one normal-equation record on the device and apply the SE(3)
+ * update to T64 (4x4 row-major fp64, in/out).  Returns status bits >= 0 or
+ * a negative YOUTH_E* code. */
+int youth_icp_solve_host(youth_icp_ctx* ctx, const double* neq, double* T64);
+
+/* --- Frame-to-frame tracking (the SLAM API's worker uses this) ----------- */
+
+/* Upload one host depth frame into the context's 2-slot ring, back-project
+ * it with normals and, when a reference frame is held, align it (source) to
+ * the reference (target) with T_init (nullable host fp64 4x4; identity if
+ * NULL).  The new frame then becomes the reference.  T_rel (host fp64 4x4):
+ * P_ref = T_rel * P_new, identity for the first frame (*has_ref = 0).
+ * Returns status bits (>= 0) or a negative YOUTH_E* code.  Synchronous. */
+int youth_icp_track_frame(youth_icp_ctx* ctx, const int16_t* depth,
+                          const double* T_init, double* T_rel, int* has_ref);
+
+/* Forget the reference frame (next tracked frame starts a new sequence). */
+void youth_icp_track_reset(youth_icp_ctx* ctx);
+
+/* --- Host utilities (no device needed) ----------------------------------- */
+
+/* Reads Camera.fx/fy/cx/cy/width/height and DepthMapFactor from an
+ * ORB-SLAM3-style YAML (astra_orb_slam3_rgbd.yaml:9-20,35).  Missing keys keep
+ * the values already in *K / *W / *H.  Returns 1 if the file was read, 0 if
+ * it could not be opened. */
+int youth_parse_camera_yaml(const char* path, youth_intrinsics* K, int* W, int* H);
+
+/* Bounded frame-ingest queue with the reference's overflow policy
+ * (SLAM.cpp:159-169: after a push, if size > high_water, drop the oldest until
+ * size == low_water; reference values 10 / 5).  Thread-safe.  Frames are
+ * copied in and out. */
+typedef struct youth_frame_queue youth_frame_queue;
+youth_frame_queue* youth_queue_create(int high_water, int low_water);
+void youth_queue_destroy(youth_frame_queue* q);
+/* Returns the number of frames dropped by this push (>= 0), or YOUTH_E*. */
+int youth_queue_push(youth_frame_queue* q, const int16_t* depth, int width,
+                     int height, uint32_t timestamp);
+/* Pops the oldest frame into depth_out (capacity `cap` int16 values).
+ * Returns 1 when a frame was popped, 0 when empty, YOUTH_EINVAL when the
+ * frame does not fit (it stays queued). */
+int youth_queue_pop(youth_frame_queue* q, int16_t* depth_out, size_t cap,
+                    int* width, int* height, uint32_t* timestamp);
+int youth_queue_size(youth_frame_queue* q);
+void youth_queue_clear(youth_frame_queue* q);
+
+/* --- SLAM-module introspection (additive) ------------------------------- */
+
+/* Number of poses in the trajectory (1 per tracked frame). */
+int youth_slam_trajectory_length(void);
+/* Copy up to n trajectory entries: timestamps [n] and world poses [n][16]
+ * (fp64 row-major, first frame = identity).  Returns the count copied. */
+int youth_slam_get_trajectory(int n, uint32_t* timestamps, double* T_wc);
+/* Block until the ingest queue is empty and the worker is idle, or
+ * timeout_ms elapses.  Returns 1 when drained, 0 on timeout / not running. */
+int youth_slam_wait_idle(int timeout_ms);
+/* Block until the module stops (used by algorithmModule). */
+void youth_slam_wait_stopped(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* YOUTH_ICP_H */

@@ -1,0 +1,355 @@
+/*
+ * icp_oracle.c — CPU ORACLE (test infrastructure only; see icp_oracle.h).
+ *
+ * Every fp32 expression below is written in the exact evaluation order the
+ * HIP kernels use (slam-rgbd_amd/csrc/icp_kernels.hip) and is compiled with
+ * -ffp-contract=off, so back-projection, normals and association indices are
+ * bit-identical between the two.  Reductions are fp64 of exact fp32
+ * products (a product of two fp32 values is exact in fp64), so CPU and GPU
+ * sums differ only by fp64 summation order.
+ */
+#include "icp_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* viewerModule.c:341-345: `if(depthValue > 0)`, `z_pos = depthValue/1000.0f`,
+ * `x_pos = (x - currentWidth/2) * z_pos / 570.3f`.  With cx = (float)(W/2)
+ * the subtraction ((float)u - cx) is exact, so this equals the viewer's
+ * (float)(u - W/2) bit-for-bit. */
+void oracle_backproject(const int16_t* depth, int W, int H,
+                        const oracle_intrinsics* K, float* X, float* Y, float* Z)
+{
+    for (int v = 0; v < H; ++v) {
+        for (int u = 0; u < W; ++u) {
+            const int i = v * W + u;
+            const int d = depth[i];
+            if (d > 0) {
+                const float z = (float)d / K->depth_scale;
+                X[i] = (((float)u - K->cx) * z) / K->fx;
+                Y[i] = (((float)v - K->cy) * z) / K->fy;
+                Z[i] = z;
+            } else {
+                X[i] = 0.0f;
+                Y[i] = 0.0f;
+                Z[i] = 0.0f;
+            }
+        }
+    }
+}
+
+void oracle_normals(const float* X, const float* Y, const float* Z, int W, int H,
+                    float* NX, float* NY, float* NZ)
+{
+    for (int v = 0; v < H; ++v) {
+        for (int u = 0; u < W; ++u) {
+            const int i = v * W + u;
+            NX[i] = 0.0f;
+            NY[i] = 0.0f;
+            NZ[i] = 0.0f;
+            if (u == 0 || v == 0 || u == W - 1 || v == H - 1) continue;
+            const int l = i - 1, r = i + 1, up = i - W, dn = i + W;
+            if (!(Z[i] > 0.0f) || !(Z[l] > 0.0f) || !(Z[r] > 0.0f) ||
+                !(Z[up] > 0.0f) || !(Z[dn] > 0.0f))
+                continue;
+            const float ax = X[r] - X[l], ay = Y[r] - Y[l], az = Z[r] - Z[l];
+            const float bx = X[dn] - X[up], by = Y[dn] - Y[up], bz = Z[dn] - Z[up];
+            const float cx = ay * bz - az * by;
+            const float cy = az * bx - ax * bz;
+            const float cz = ax * by - ay * bx;
+            const float len2 = (cx * cx + cy * cy) + cz * cz;
+            if (!(len2 > 0.0f)) continue;
+            const float len = sqrtf(len2);
+            float nx = cx / len, ny = cy / len, nz = cz / len;
+            if (((nx * X[i] + ny * Y[i]) + nz * Z[i]) > 0.0f) {
+                nx = -nx;
+                ny = -ny;
+                nz = -nz;
+            }
+            NX[i] = nx;
+            NY[i] = ny;
+            NZ[i] = nz;
+        }
+    }
+}
+
+/* Spec a7 for one source point.  Returns the target index or -1 and, when
+ * matched, the transformed point q. */
+static inline int assoc_one(float sx, float sy, float sz, const float T[12],
+                            const oracle_intrinsics* K, int W, int H,
+                            const float* tX, const float* tY, const float* tZ,
+                            const float* nX, const float* nY, const float* nZ,
+                            float thr2, float q[3])
+{
+    if (!(sz > 0.0f)) return -1;
+    const float qx = ((T[0] * sx + T[1] * sy) + T[2] * sz) + T[3];
+    const float qy = ((T[4] * sx + T[5] * sy) + T[6] * sz) + T[7];
+    const float qz = ((T[8] * sx + T[9] * sy) + T[10] * sz) + T[11];
+    if (!(qz > 0.0f)) return -1;
+    const float fu = floorf((((K->fx * qx) / qz) + K->cx) + 0.5f);
+    const float fv = floorf((((K->fy * qy) / qz) + K->cy) + 0.5f);
+    if (!(fu >= 0.0f && fu < (float)W && fv >= 0.0f && fv < (float)H)) return -1;
+    const int j = (int)fv * W + (int)fu;
+    const float tz = tZ[j];
+    if (!(tz > 0.0f)) return -1;
+    if (nX[j] == 0.0f && nY[j] == 0.0f && nZ[j] == 0.0f) return -1;
+    const float dx = qx - tX[j], dy = qy - tY[j], dz = qz - tz;
+    const float d2 = (dx * dx + dy * dy) + dz * dz;
+    if (!(d2 < thr2)) return -1;
+    q[0] = qx;
+    q[1] = qy;
+    q[2] = qz;
+    return j;
+}
+
+void oracle_associate(const float* sX, const float* sY, const float* sZ,
+                      const float* tX, const float* tY, const float* tZ,
+                      const float* nX, const float* nY, const float* nZ,
+                      int W, int H, const oracle_intrinsics* K, const float T[12],
+                      float dist_thresh, int32_t* idx)
+{
+    const float thr2 = dist_thresh * dist_thresh;
+    const int N = W * H;
+    float q[3];
+    for (int i = 0; i < N; ++i)
+        idx[i] = assoc_one(sX[i], sY[i], sZ[i], T, K, W, H, tX, tY, tZ, nX, nY,
+                           nZ, thr2, q);
+}
+
+void oracle_reduce(const float* sX, const float* sY, const float* sZ,
+                   const float* tX, const float* tY, const float* tZ,
+                   const float* nX, const float* nY, const float* nZ,
+                   int W, int H, const oracle_intrinsics* K, const float T[12],
+                   float dist_thresh, double out[ORACLE_NEQ])
+{
+    const float thr2 = dist_thresh * dist_thresh;
+    const int N = W * H;
+    double acc[ORACLE_NEQ];
+    memset(acc, 0, sizeof(acc));
+    float q[3];
+    for (int i = 0; i < N; ++i) {
+        const int j = assoc_one(sX[i], sY[i], sZ[i], T, K, W, H, tX, tY, tZ, nX,
+                                nY, nZ, thr2, q);
+        if (j < 0) continue;
+        const float nx = nX[j], ny = nY[j], nz = nZ[j];
+        const float dx = q[0] - tX[j], dy = q[1] - tY[j], dz = q[2] - tZ[j];
+        /* residual r = n . (P' - P_t)  (spec a8) */
+        const float r = (nx * dx + ny * dy) + nz * dz;
+        /* J = [ (P' x n)^T , n^T ]  for the left perturbation exp(xi) T */
+        float J[6];
+        J[0] = q[1] * nz - q[2] * ny;
+        J[1] = q[2] * nx - q[0] * nz;
+        J[2] = q[0] * ny - q[1] * nx;
+        J[3] = nx;
+        J[4] = ny;
+        J[5] = nz;
+        int k = 0;
+        for (int a = 0; a < 6; ++a)
+            for (int b = a; b < 6; ++b)
+                acc[k++] += (double)J[a] * (double)J[b];
+        for (int a = 0; a < 6; ++a) acc[21 + a] += (double)J[a] * (double)r;
+        acc[27] += (double)r * (double)r;
+        acc[28] += 1.0;
+    }
+    memcpy(out, acc, sizeof(acc));
+}
+
+int oracle_solve(const double neq[ORACLE_NEQ], double xi[6])
+{
+    for (int i = 0; i < 6; ++i) xi[i] = 0.0;
+    if (!(neq[28] >= 6.0)) return 2;
+    double A[6][6];
+    int k = 0;
+    for (int a = 0; a < 6; ++a)
+        for (int b = a; b < 6; ++b) {
+            A[a][b] = neq[k];
+            A[b][a] = neq[k];
+            ++k;
+        }
+    double maxd = 0.0;
+    for (int a = 0; a < 6; ++a)
+        if (A[a][a] > maxd) maxd = A[a][a];
+    if (!(maxd > 0.0)) return 1;
+    const double eps = 1e-12 * maxd;
+    double L[6][6], D[6];
+    memset(L, 0, sizeof(L));
+    for (int j = 0; j < 6; ++j) {
+        double d = A[j][j];
+        for (int m = 0; m < j; ++m) d -= (L[j][m] * L[j][m]) * D[m];
+        if (!(d > eps)) return 1;
+        D[j] = d;
+        L[j][j] = 1.0;
+        for (int i = j + 1; i < 6; ++i) {
+            double s = A[i][j];
+            for (int m = 0; m < j; ++m) s -= (L[i][m] * L[j][m]) * D[m];
+            L[i][j] = s / d;
+        }
+    }
+    double y[6], x[6];
+    for (int i = 0; i < 6; ++i) {
+        double s = -neq[21 + i];
+        for (int m = 0; m < i; ++m) s -= L[i][m] * y[m];
+        y[i] = s;
+    }
+    for (int i = 0; i < 6; ++i) y[i] = y[i] / D[i];
+    for (int i = 5; i >= 0; --i) {
+        double s = y[i];
+        for (int m = i + 1; m < 6; ++m) s -= L[m][i] * x[m];
+        x[i] = s;
+    }
+    for (int i = 0; i < 6; ++i) xi[i] = x[i];
+    return 0;
+}
+
+void oracle_se3_exp(const double xi[6], double E[16])
+{
+    const double wx = xi[0], wy = xi[1], wz = xi[2];
+    const double th2 = (wx * wx + wy * wy) + wz * wz;
+    double a, b, c;
+    if (th2 < 1e-10) {
+        a = 1.0 - th2 / 6.0;
+        b = 0.5 - th2 / 24.0;
+        c = 1.0 / 6.0 - th2 / 120.0;
+    } else {
+        const double th = sqrt(th2);
+        const double s = sin(th), co = cos(th);
+        a = s / th;
+        b = (1.0 - co) / th2;
+        c = (th - s) / (th2 * th);
+    }
+    const double Km[3][3] = {{0.0, -wz, wy}, {wz, 0.0, -wx}, {-wy, wx, 0.0}};
+    double K2[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            K2[i][j] = (Km[i][0] * Km[0][j] + Km[i][1] * Km[1][j]) + Km[i][2] * Km[2][j];
+    double R[3][3], V[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            const double I = (i == j) ? 1.0 : 0.0;
+            R[i][j] = (I + a * Km[i][j]) + b * K2[i][j];
+            V[i][j] = (I + b * Km[i][j]) + c * K2[i][j];
+        }
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) E[i * 4 + j] = R[i][j];
+        E[i * 4 + 3] = (V[i][0] * xi[3] + V[i][1] * xi[4]) + V[i][2] * xi[5];
+    }
+    E[12] = 0.0;
+    E[13] = 0.0;
+    E[14] = 0.0;
+    E[15] = 1.0;
+}
+
+/* T <- E * T (4x4 row-major; last row of both is [0 0 0 1]). */
+static void left_compose(const double E[16], double T[16])
+{
+    double O[16];
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 4; ++j) {
+            double s = (E[i * 4 + 0] * T[0 * 4 + j] + E[i * 4 + 1] * T[1 * 4 + j]) +
+                       E[i * 4 + 2] * T[2 * 4 + j];
+            if (j == 3) s += E[i * 4 + 3];
+            O[i * 4 + j] = s;
+        }
+    }
+    O[12] = 0.0;
+    O[13] = 0.0;
+    O[14] = 0.0;
+    O[15] = 1.0;
+    memcpy(T, O, sizeof(O));
+}
+
+static void to_f32(const double T[16], float T32[12])
+{
+    for (int i = 0; i < 12; ++i) T32[i] = (float)T[i];
+}
+
+static int align_ws(const int16_t* src, const int16_t* dst, int W, int H,
+                    const oracle_intrinsics* K, int iters, float dist_thresh,
+                    const double* T_init, double T64[16], float T32[12],
+                    double* stats, float* ws)
+{
+    const size_t N = (size_t)W * (size_t)H;
+    float *sX = ws, *sY = ws + N, *sZ = ws + 2 * N;
+    float *tX = ws + 3 * N, *tY = ws + 4 * N, *tZ = ws + 5 * N;
+    float *nX = ws + 6 * N, *nY = ws + 7 * N, *nZ = ws + 8 * N;
+    oracle_backproject(src, W, H, K, sX, sY, sZ);
+    oracle_backproject(dst, W, H, K, tX, tY, tZ);
+    oracle_normals(tX, tY, tZ, W, H, nX, nY, nZ);
+    double T[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    if (T_init) memcpy(T, T_init, sizeof(T));
+    int status = 0;
+    for (int it = 0; it < iters; ++it) {
+        float Tf[12];
+        to_f32(T, Tf);
+        double neq[ORACLE_NEQ], xi[6], E[16];
+        oracle_reduce(sX, sY, sZ, tX, tY, tZ, nX, nY, nZ, W, H, K, Tf, dist_thresh,
+                      neq);
+        if (stats) {
+            stats[2 * it + 0] = neq[28];
+            stats[2 * it + 1] = neq[27];
+        }
+        const int st = oracle_solve(neq, xi);
+        status |= st;
+        if (st == 0) {
+            oracle_se3_exp(xi, E);
+            left_compose(E, T);
+        }
+    }
+    memcpy(T64, T, sizeof(T));
+    to_f32(T, T32);
+    return status;
+}
+
+int oracle_align(const int16_t* src, const int16_t* dst, int W, int H,
+                 const oracle_intrinsics* K, int iters, float dist_thresh,
+                 const double* T_init, double T64[16], float T32[12],
+                 double* stats)
+{
+    const size_t N = (size_t)W * (size_t)H;
+    float* ws = (float*)malloc(9 * N * sizeof(float));
+    if (!ws) return -1;
+    const int st = align_ws(src, dst, W, H, K, iters, dist_thresh, T_init, T64,
+                            T32, stats, ws);
+    free(ws);
+    return st;
+}
+
+void oracle_align_batch(const int16_t* src, const int16_t* dst, int n_pairs,
+                        int W, int H, const oracle_intrinsics* K, int iters,
+                        float dist_thresh, double* T64, int32_t* status,
+                        int n_threads)
+{
+    const size_t N = (size_t)W * (size_t)H;
+#ifdef _OPENMP
+    if (n_threads <= 0) n_threads = omp_get_max_threads();
+#pragma omp parallel num_threads(n_threads)
+#endif
+    {
+        float* ws = (float*)malloc(9 * N * sizeof(float));
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+        for (int p = 0; p < n_pairs; ++p) {
+            float T32[12];
+            status[p] = ws ? align_ws(src + (size_t)p * N, dst + (size_t)p * N, W, H,
+                                      K, iters, dist_thresh, NULL,
+                                      T64 + (size_t)p * 16, T32, NULL, ws)
+                           : -1;
+        }
+        free(ws);
+    }
+    (void)n_threads;
+}
+
+int oracle_max_threads(void)
+{
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}

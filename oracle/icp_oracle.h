@@ -1,0 +1,103 @@
+/*
+ * icp_oracle.h — CPU ORACLE for the RGBD frame-to-frame ICP path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the shipped library links, loads or
+ * calls this code; only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may use it, and only as the checker / timed CPU baseline.
+ *
+ * What it restates (reference = SeunghwanByun/SLAM-RGBD @ 2025-08-24):
+ *   - back-projection: Youth.Source/ViewerModule/viewerModule.c:341-345
+ *     (valid iff d > 0; Z = d/1000.0f; X = ((u - W/2) * Z)/570.3f; Y alike),
+ *     generalised to explicit intrinsics that reproduce the viewer bit-for-bit
+ *     when cx = W/2, cy = H/2, fx = fy = 570.3f, depth_scale = 1000.0f;
+ *   - intrinsics / depth factor: AlgorithmModule/config/astra_orb_slam3_rgbd.yaml:9-12,35;
+ *   - buffer layout int16 [H][W] row-major: SLAM.h:22, frameDefinitions.h:11-20.
+ * PINNED against the back-projection known-answer table of SURVEY.md §4
+ * (bit patterns computed with gcc -O2 -ffp-contract=off, x86-64 SSE fp32) —
+ * see tests/test_oracle.py.
+ *
+ * PARITY UNPINNED for everything after back-projection: the reference has no
+ * ICP (its pose maths is inside un-vendored ORB-SLAM3,
+ * SLAM.cpp:54, version unpinned, feature-based).  Normals, projective
+ * association, point-to-plane Jacobian, 6x6 reduction, LDL^T solve and the
+ * SE(3) update follow this build's own spec (SURVEY.md §8a rows a6-a10,
+ * DESIGN.md §2), checked here against numpy/scipy and known-motion recovery.
+ *
+ * Build: gcc -O2 -ffp-contract=off (no -ffast-math, no -march=native), so
+ * every fp32 expression rounds exactly as written — the GPU kernels are
+ * compiled with the same contraction rule and must match bit-for-bit on XYZ,
+ * normals and association indices.
+ */
+#ifndef YOUTH_ICP_ORACLE_H
+#define YOUTH_ICP_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct oracle_intrinsics {
+    float fx, fy, cx, cy, depth_scale;
+} oracle_intrinsics; /* layout-identical to youth_intrinsics */
+
+#define ORACLE_NEQ 29
+
+/* viewerModule.c:341-345 generalised.  Invalid pixel -> X=Y=Z=0. */
+void oracle_backproject(const int16_t* depth, int W, int H,
+                        const oracle_intrinsics* K, float* X, float* Y, float* Z);
+
+/* Central-difference normals (spec a6): n = normalize((P(u+1)-P(u-1)) x
+ * (P(v+1)-P(v-1))), invalid (0,0,0) on the 1-px border, if any of the 4
+ * neighbours or the centre is invalid, or the cross product is zero;
+ * oriented so n.P <= 0. */
+void oracle_normals(const float* X, const float* Y, const float* Z, int W, int H,
+                    float* NX, float* NY, float* NZ);
+
+/* Projective association (spec a7) for every source pixel at the fp32 pose
+ * T (3x4 row-major, P' = R P + t).  idx[i] = v'*W+u' or -1. */
+void oracle_associate(const float* sX, const float* sY, const float* sZ,
+                      const float* tX, const float* tY, const float* tZ,
+                      const float* nX, const float* nY, const float* nZ,
+                      int W, int H, const oracle_intrinsics* K, const float T[12],
+                      float dist_thresh, int32_t* idx);
+
+/* Point-to-plane normal equations (spec a8-a9) at pose T, accumulated in
+ * fp64 in row-major pixel order.  out[29] as YOUTH_NEQ. */
+void oracle_reduce(const float* sX, const float* sY, const float* sZ,
+                   const float* tX, const float* tY, const float* tZ,
+                   const float* nX, const float* nY, const float* nZ,
+                   int W, int H, const oracle_intrinsics* K, const float T[12],
+                   float dist_thresh, double out[ORACLE_NEQ]);
+
+/* LDL^T solve of A xi = -b (spec a10).  Returns 0, or status bits
+ * (1 = singular pivot, 2 = fewer than 6 correspondences); xi zeroed then. */
+int oracle_solve(const double neq[ORACLE_NEQ], double xi[6]);
+
+/* SE(3) exponential of xi = (omega, upsilon), 4x4 row-major fp64. */
+void oracle_se3_exp(const double xi[6], double E[16]);
+
+/* Full align of one pair: back-project both, target normals, `iters` fixed
+ * iterations T <- exp(xi) T.  T_init nullable (identity).  Outputs: T64
+ * [16], T32 [12] (the fp32 pose used by the NEXT iteration), stats
+ * nullable [iters][2] (count, sum r^2).  Returns accumulated status bits. */
+int oracle_align(const int16_t* src, const int16_t* dst, int W, int H,
+                 const oracle_intrinsics* K, int iters, float dist_thresh,
+                 const double* T_init, double T64[16], float T32[12],
+                 double* stats);
+
+/* Batch of independent pairs, OpenMP over pairs with n_threads threads
+ * (<= 0: all).  src/dst [n][H][W]; T64 [n][16]; status [n]. */
+void oracle_align_batch(const int16_t* src, const int16_t* dst, int n_pairs,
+                        int W, int H, const oracle_intrinsics* K, int iters,
+                        float dist_thresh, double* T64, int32_t* status,
+                        int n_threads);
+
+/* Threads OpenMP will use for n_threads <= 0 (1 when built without OpenMP). */
+int oracle_max_threads(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

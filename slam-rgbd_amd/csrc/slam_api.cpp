@@ -1,0 +1,487 @@
+// slam_api.cpp — drop-in implementation of the reference's SLAM.h C API.
+//
+// Reference: Youth.Source/AlgorithmModule/SLAM.h:11-38 and SLAM.cpp:15-230.
+// Same entry points, argument meaning, 1/0 return convention and threading
+// model (caller threads enqueue; ONE private worker thread tracks), but the
+// ORB-SLAM3 TrackRGBD call (SLAM.cpp:54) is replaced by HIP frame-to-frame
+// point-to-plane ICP (youth_icp_track_frame).  Host-only C++: no HIP types.
+//
+// Differences from the reference that are deliberate:
+//  - processSlamFrame keeps depth as int16 millimetres (the GPU converts with
+//    the viewer's /1000.0f rule, viewerModule.c:343) instead of
+//    convertTo(CV_32F, 1/1000) (SLAM.cpp:154-155); colour is ignored (ICP).
+//  - every frame path returns a value (SLAM.cpp:172-174 falls off the end).
+//  - the running flags are atomics (the reference shares plain bools).
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "youth_icp.h"
+
+// ------------------------------------------------------- ingest queue -----
+struct youth_frame_queue {
+    struct Item {
+        std::vector<int16_t> depth;
+        int w, h;
+        uint32_t ts;
+    };
+    std::mutex mu;
+    std::deque<Item> q;
+    int high = 10, low = 5;
+};
+
+extern "C" {
+
+youth_frame_queue* youth_queue_create(int high_water, int low_water)
+{
+    if (high_water < 1 || low_water < 0 || low_water > high_water) return nullptr;
+    auto* q = new youth_frame_queue();
+    q->high = high_water;
+    q->low = low_water;
+    return q;
+}
+
+void youth_queue_destroy(youth_frame_queue* q) { delete q; }
+
+int youth_queue_push(youth_frame_queue* q, const int16_t* depth, int width, int height,
+                     uint32_t timestamp)
+{
+    if (!q || !depth || width <= 0 || height <= 0) return YOUTH_EINVAL;
+    youth_frame_queue::Item it;
+    try {
+        it.depth.assign(depth, depth + (size_t)width * (size_t)height);
+    } catch (...) {
+        return YOUTH_ENOMEM;
+    }
+    it.w = width;
+    it.h = height;
+    it.ts = timestamp;
+    std::lock_guard<std::mutex> lk(q->mu);
+    q->q.push_back(std::move(it));
+    int dropped = 0;
+    // SLAM.cpp:163-168: size > 10 -> pop the oldest down to 5
+    if ((int)q->q.size() > q->high) {
+        fprintf(stderr, "youth_icp: frame queue is getting large (%zu), dropping to %d\n",
+                q->q.size(), q->low);
+        while ((int)q->q.size() > q->low) {
+            q->q.pop_front();
+            ++dropped;
+        }
+    }
+    return dropped;
+}
+
+int youth_queue_pop(youth_frame_queue* q, int16_t* depth_out, size_t cap, int* width,
+                    int* height, uint32_t* timestamp)
+{
+    if (!q) return YOUTH_EINVAL;
+    std::lock_guard<std::mutex> lk(q->mu);
+    if (q->q.empty()) return 0;
+    auto& it = q->q.front();
+    if (it.depth.size() > cap || !depth_out) return YOUTH_EINVAL;
+    memcpy(depth_out, it.depth.data(), it.depth.size() * sizeof(int16_t));
+    if (width) *width = it.w;
+    if (height) *height = it.h;
+    if (timestamp) *timestamp = it.ts;
+    q->q.pop_front();
+    return 1;
+}
+
+int youth_queue_size(youth_frame_queue* q)
+{
+    if (!q) return 0;
+    std::lock_guard<std::mutex> lk(q->mu);
+    return (int)q->q.size();
+}
+
+void youth_queue_clear(youth_frame_queue* q)
+{
+    if (!q) return;
+    std::lock_guard<std::mutex> lk(q->mu);
+    q->q.clear();
+}
+
+// ---------------------------------------------------------- YAML config ---
+int youth_parse_camera_yaml(const char* path, youth_intrinsics* K, int* W, int* H)
+{
+    if (!path || !K) return 0;
+    FILE* f = fopen(path, "r");
+    if (!f) return 0;
+    char line[512];
+    while (fgets(line, sizeof(line), f)) {
+        char* p = line;
+        while (*p == ' ' || *p == '\t') ++p;
+        if (*p == '#' || *p == '\0' || *p == '\n') continue;
+        char* colon = strchr(p, ':');
+        if (!colon) continue;
+        std::string key(p, colon - p);
+        while (!key.empty() && (key.back() == ' ' || key.back() == '\t')) key.pop_back();
+        char* end = nullptr;
+        const double val = strtod(colon + 1, &end);
+        if (end == colon + 1) continue;  // not a number (e.g. Camera.type: "PinHole")
+        if (key == "Camera.fx") K->fx = (float)val;
+        else if (key == "Camera.fy") K->fy = (float)val;
+        else if (key == "Camera.cx") K->cx = (float)val;
+        else if (key == "Camera.cy") K->cy = (float)val;
+        else if (key == "DepthMapFactor") K->depth_scale = (float)val;
+        else if (key == "Camera.width" && W) *W = (int)val;
+        else if (key == "Camera.height" && H) *H = (int)val;
+    }
+    fclose(f);
+    return 1;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------ SLAM state --
+namespace {
+
+struct PoseRec {
+    uint32_t ts;
+    double T[16];
+};
+
+std::mutex g_slam_mu;  // SLAM.cpp:16 slam_mutex: tracker + trajectory
+std::atomic<bool> g_running{false};
+std::atomic<bool> g_process{false};  // SLAM.cpp:29 process_frames
+std::atomic<bool> g_busy{false};
+std::atomic<bool> g_reset{false};
+std::thread g_worker;
+youth_frame_queue* g_queue = nullptr;
+
+std::mutex g_state_mu;  // run/stop hand-off for algorithmModule
+std::condition_variable g_state_cv;
+
+// configuration from initSlamModule
+youth_intrinsics g_cfg_K;
+int g_cfg_W = 0, g_cfg_H = 0;
+bool g_cfg_has_yaml = false;
+
+// tracker state (worker thread owns ctx; trajectory guarded by g_slam_mu)
+std::vector<PoseRec> g_traj;
+int g_last_points = 0;
+
+void mat_mul4(const double* A, const double* B, double* C)
+{
+    double O[16];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            double s = 0.0;
+            for (int k = 0; k < 4; ++k) s += A[i * 4 + k] * B[k * 4 + j];
+            O[i * 4 + j] = s;
+        }
+    memcpy(C, O, sizeof(O));
+}
+
+youth_intrinsics intrinsics_for(int w, int h)
+{
+    if (g_cfg_has_yaml && (g_cfg_W == 0 || g_cfg_W == w) && (g_cfg_H == 0 || g_cfg_H == h))
+        return g_cfg_K;
+    return youth_default_intrinsics(w, h);
+}
+
+// SLAM.cpp:32-63 processFramesThread, with TrackRGBD replaced by HIP ICP.
+void worker_main(int device)
+{
+    fprintf(stderr, "youth_icp: SLAM processing thread started\n");
+    youth_icp_ctx* ctx = nullptr;
+    int cw = 0, ch = 0;
+    std::vector<int16_t> buf;
+    double T_w_ref[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    while (g_process.load()) {
+        if (buf.empty()) buf.resize((size_t)4096 * 4096);
+        int w = 0, h = 0;
+        uint32_t ts = 0;
+        g_busy.store(true);
+        const int got = youth_queue_pop(g_queue, buf.data(), buf.size(), &w, &h, &ts);
+        if (got != 1) {
+            g_busy.store(false);
+            std::this_thread::sleep_for(std::chrono::milliseconds(got == 0 ? 1 : 5));
+            continue;
+        }
+        if (g_reset.exchange(false) && ctx) youth_icp_track_reset(ctx);
+        if (!ctx || w != cw || h != ch) {
+            if (ctx) youth_icp_destroy(ctx);
+            const youth_intrinsics K = intrinsics_for(w, h);
+            ctx = youth_icp_create(device, w, h, 2, &K, nullptr);
+            cw = w;
+            ch = h;
+            if (!ctx) {
+                fprintf(stderr, "youth_icp: context creation failed: %s\n",
+                        youth_icp_last_error());
+                cw = ch = 0;
+                g_busy.store(false);
+                continue;
+            }
+        }
+        double T_rel[16];
+        int has_ref = 0;
+        const int st = youth_icp_track_frame(ctx, buf.data(), nullptr, T_rel, &has_ref);
+        if (st < 0) {
+            fprintf(stderr, "youth_icp: tracking failed: %s\n", youth_icp_last_error());
+            g_busy.store(false);
+            continue;
+        }
+        int npts = 0;
+        for (size_t i = 0; i < (size_t)w * h; ++i) npts += buf[i] > 0;
+        {
+            std::lock_guard<std::mutex> lk(g_slam_mu);
+            if (!has_ref || g_traj.empty()) {
+                // new sequence: this frame is the world origin
+                double I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+                memcpy(T_w_ref, I, sizeof(I));
+                g_traj.clear();
+            } else {
+                // P_ref = T_rel P_new  =>  T_w_new = T_w_ref * T_rel
+                mat_mul4(T_w_ref, T_rel, T_w_ref);
+            }
+            PoseRec pr;
+            pr.ts = ts;
+            memcpy(pr.T, T_w_ref, sizeof(pr.T));
+            g_traj.push_back(pr);
+            g_last_points = npts;
+        }
+        g_busy.store(false);
+    }
+    if (ctx) youth_icp_destroy(ctx);
+    fprintf(stderr, "youth_icp: SLAM processing thread stopped\n");
+}
+
+// Rotation matrix -> unit quaternion (x, y, z, w), Shepperd's method.
+void rot_to_quat(const double* T, double q[4])
+{
+    const double m00 = T[0], m01 = T[1], m02 = T[2];
+    const double m10 = T[4], m11 = T[5], m12 = T[6];
+    const double m20 = T[8], m21 = T[9], m22 = T[10];
+    const double tr = m00 + m11 + m22;
+    double x, y, z, w;
+    if (tr > 0.0) {
+        const double s = std::sqrt(tr + 1.0) * 2.0;
+        w = 0.25 * s;
+        x = (m21 - m12) / s;
+        y = (m02 - m20) / s;
+        z = (m10 - m01) / s;
+    } else if (m00 > m11 && m00 > m22) {
+        const double s = std::sqrt(1.0 + m00 - m11 - m22) * 2.0;
+        w = (m21 - m12) / s;
+        x = 0.25 * s;
+        y = (m01 + m10) / s;
+        z = (m02 + m20) / s;
+    } else if (m11 > m22) {
+        const double s = std::sqrt(1.0 + m11 - m00 - m22) * 2.0;
+        w = (m02 - m20) / s;
+        x = (m01 + m10) / s;
+        y = 0.25 * s;
+        z = (m12 + m21) / s;
+    } else {
+        const double s = std::sqrt(1.0 + m22 - m00 - m11) * 2.0;
+        w = (m10 - m01) / s;
+        x = (m02 + m20) / s;
+        y = (m12 + m21) / s;
+        z = 0.25 * s;
+    }
+    const double n = std::sqrt(x * x + y * y + z * z + w * w);
+    q[0] = x / n;
+    q[1] = y / n;
+    q[2] = z / n;
+    q[3] = w / n;
+}
+
+int write_tum(const std::string& path, const std::vector<PoseRec>& traj)
+{
+    FILE* f = fopen(path.c_str(), "w");
+    if (!f) return 0;
+    for (const auto& p : traj) {
+        double q[4];
+        rot_to_quat(p.T, q);
+        // the reference hands TrackRGBD the ms timestamp as "seconds"
+        // (SLAM.cpp:151), so the TUM time column carries ms as-is.
+        fprintf(f, "%.6f %.9f %.9f %.9f %.9f %.9f %.9f %.9f\n", (double)p.ts, p.T[3], p.T[7],
+                p.T[11], q[0], q[1], q[2], q[3]);
+    }
+    const int ok = ferror(f) == 0;
+    fclose(f);
+    return ok;
+}
+
+}  // namespace
+
+extern "C" {
+
+// SLAM.cpp:67-95
+void initSlamModule(const char* config_file, const char* vocabulary_file)
+{
+    (void)vocabulary_file;  // no ORB vocabulary in an ICP tracker
+    fprintf(stderr, "youth_icp: initializing HIP ICP module...\n");
+    if (g_running.load()) {
+        fprintf(stderr, "youth_icp: SLAM module is already running\n");
+        return;
+    }
+    std::lock_guard<std::mutex> lk(g_slam_mu);
+    const int ndev = youth_icp_device_count();
+    if (ndev <= 0) {
+        // the product path never falls back to a CPU tracker
+        fprintf(stderr, "youth_icp: no HIP device visible; module NOT started\n");
+        return;
+    }
+    g_cfg_K = youth_default_intrinsics(640, 480);
+    g_cfg_W = 0;
+    g_cfg_H = 0;
+    g_cfg_has_yaml = false;
+    if (config_file && youth_parse_camera_yaml(config_file, &g_cfg_K, &g_cfg_W, &g_cfg_H))
+        g_cfg_has_yaml = true;
+    else if (config_file)
+        fprintf(stderr, "youth_icp: cannot read %s; using viewer intrinsics\n", config_file);
+    int device = 0;
+    if (const char* e = getenv("YOUTH_ICP_DEVICE")) device = atoi(e);
+    if (device < 0 || device >= ndev) device = 0;
+    if (!g_queue) g_queue = youth_queue_create(10, 5);
+    youth_queue_clear(g_queue);
+    g_traj.clear();
+    g_last_points = 0;
+    g_process.store(true);
+    try {
+        g_worker = std::thread(worker_main, device);
+    } catch (const std::exception& ex) {
+        fprintf(stderr, "youth_icp: failed to start worker: %s\n", ex.what());
+        g_process.store(false);
+        return;
+    }
+    {
+        std::lock_guard<std::mutex> sl(g_state_mu);
+        g_running.store(true);
+    }
+    g_state_cv.notify_all();
+    fprintf(stderr, "youth_icp: HIP ICP module initialized (device %d)\n", device);
+}
+
+// SLAM.cpp:97-124
+void stopSlamModule(void)
+{
+    fprintf(stderr, "youth_icp: stopping HIP ICP module...\n");
+    g_process.store(false);
+    if (g_worker.joinable()) g_worker.join();
+    if (g_queue) youth_queue_clear(g_queue);
+    {
+        std::lock_guard<std::mutex> sl(g_state_mu);
+        g_running.store(false);
+    }
+    g_state_cv.notify_all();
+    fprintf(stderr, "youth_icp: HIP ICP module stopped\n");
+}
+
+// SLAM.cpp:126-175
+int processSlamFrame(const int16_t* depth_data, const uint8_t* color_data, int width,
+                     int height, uint32_t timestamp)
+{
+    (void)color_data;
+    if (!g_running.load() || !g_queue) return 0;
+    if (!depth_data || width < 3 || height < 3 || width > 4096 || height > 4096) {
+        fprintf(stderr, "youth_icp: processSlamFrame: bad frame %dx%d\n", width, height);
+        return 0;
+    }
+    const int rc = youth_queue_push(g_queue, depth_data, width, height, timestamp);
+    if (rc < 0) {
+        fprintf(stderr, "youth_icp: processSlamFrame: enqueue failed (%d)\n", rc);
+        return 0;
+    }
+    return 1;
+}
+
+// SLAM.cpp:177-198
+int saveSlamMap(const char* map_file)
+{
+    if (!g_running.load() || !map_file) {
+        fprintf(stderr, "youth_icp: SLAM system is not running\n");
+        return 0;
+    }
+    std::vector<PoseRec> traj;
+    {
+        std::lock_guard<std::mutex> lk(g_slam_mu);
+        traj = g_traj;
+    }
+    const std::string base(map_file);
+    // every frame is tracked frame-to-frame, so the keyframe file equals the
+    // trajectory (SLAM.cpp:188 writes both)
+    const int ok = write_tum(base + "_trajectory.txt", traj) &&
+                   write_tum(base + "_keyframes.txt", traj);
+    if (ok)
+        fprintf(stderr, "youth_icp: map saved to %s\n", map_file);
+    else
+        fprintf(stderr, "youth_icp: error saving map to %s\n", map_file);
+    return ok ? 1 : 0;
+}
+
+int isSlamModuleRunning(void) { return g_running.load() ? 1 : 0; }
+
+int getSlamMapPoints(void)
+{
+    if (!g_running.load()) return 0;
+    std::lock_guard<std::mutex> lk(g_slam_mu);
+    return g_last_points;
+}
+
+void resetSlam(void)
+{
+    if (!g_running.load()) return;
+    {
+        std::lock_guard<std::mutex> lk(g_slam_mu);
+        g_traj.clear();
+        g_last_points = 0;
+    }
+    g_reset.store(true);
+    fprintf(stderr, "youth_icp: SLAM system reset\n");
+}
+
+int youth_slam_trajectory_length(void)
+{
+    std::lock_guard<std::mutex> lk(g_slam_mu);
+    return (int)g_traj.size();
+}
+
+int youth_slam_get_trajectory(int n, uint32_t* timestamps, double* T_wc)
+{
+    std::lock_guard<std::mutex> lk(g_slam_mu);
+    int m = (int)g_traj.size();
+    if (n < m) m = n;
+    for (int i = 0; i < m; ++i) {
+        if (timestamps) timestamps[i] = g_traj[i].ts;
+        if (T_wc) memcpy(T_wc + (size_t)i * 16, g_traj[i].T, sizeof(g_traj[i].T));
+    }
+    return m;
+}
+
+int youth_slam_wait_idle(int timeout_ms)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    while (g_running.load()) {
+        if (youth_queue_size(g_queue) == 0 && !g_busy.load()) {
+            // re-check after a short pause: the worker may be between pop and busy
+            std::this_thread::sleep_for(std::chrono::milliseconds(2));
+            if (youth_queue_size(g_queue) == 0 && !g_busy.load()) return 1;
+        }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms))
+            return 0;
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+    return 0;
+}
+
+void youth_slam_wait_stopped(void)
+{
+    std::unique_lock<std::mutex> lk(g_state_mu);
+    g_state_cv.wait(lk, [] { return !g_running.load(); });
+}
+
+}  // extern "C"

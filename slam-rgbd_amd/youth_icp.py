@@ -1,0 +1,389 @@
+"""Python host mirror of the C-ABI in include/youth_icp.h (ctypes, no torch).
+
+Two layers, mirroring the reference's interface for this path:
+
+* The reference's own AlgorithmModule API — same names, argument meaning and
+  1/0 return convention as Youth.Source/AlgorithmModule/SLAM.h:11-38
+  (``initSlamModule``, ``stopSlamModule``, ``processSlamFrame``,
+  ``saveSlamMap``, ``isSlamModuleRunning``, ``getSlamMapPoints``,
+  ``resetSlam``) so a parity test reads like a caller of SLAM.h.
+* The additive batch / device API (``IcpContext``, ``align_batch``).
+
+The library is built in-tree (``make -C slam-rgbd_amd``) and loaded from
+next to this file.  There is no CPU fallback: if ``libyouth_icp.so`` is
+missing, importing the wrappers raises, and every compute call on a machine
+without a HIP device returns ``YOUTH_ENODEV`` -> ``IcpError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int16, c_int32
+from ctypes import c_size_t, c_uint8, c_uint32, c_void_p
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libyouth_icp.so")
+HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "youth_icp.h")
+
+YOUTH_OK = 0
+YOUTH_EINVAL = -1
+YOUTH_ENOMEM = -2
+YOUTH_EHIP = -3
+YOUTH_ENODEV = -4
+YOUTH_NEQ = 29
+STATUS_DEGENERATE = 1
+STATUS_FEW_MATCHES = 2
+
+
+class IcpError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"youth_icp error {code}: {msg}")
+        self.code = code
+
+
+class Intrinsics(ctypes.Structure):
+    _fields_ = [("fx", c_float), ("fy", c_float), ("cx", c_float), ("cy", c_float),
+                ("depth_scale", c_float)]
+
+    def as_tuple(self):
+        return (self.fx, self.fy, self.cx, self.cy, self.depth_scale)
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("iters", c_int), ("dist_thresh", c_float)]
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libyouth_icp.so (raises OSError when it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise OSError(f"{path} not built: run `make -C {HERE}` (HIP extension missing)")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    P16, PU8, PF, PD, PI32 = POINTER(c_int16), POINTER(c_uint8), POINTER(c_float), \
+        POINTER(c_double), POINTER(c_int32)
+    sig = {
+        "initSlamModule": (None, [c_char_p, c_char_p]),
+        "stopSlamModule": (None, []),
+        "processSlamFrame": (c_int, [P16, PU8, c_int, c_int, c_uint32]),
+        "saveSlamMap": (c_int, [c_char_p]),
+        "isSlamModuleRunning": (c_int, []),
+        "getSlamMapPoints": (c_int, []),
+        "resetSlam": (None, []),
+        "algorithmModule": (c_void_p, [c_void_p]),
+        "youth_default_intrinsics": (Intrinsics, [c_int, c_int]),
+        "youth_default_params": (Params, []),
+        "youth_icp_last_error": (c_char_p, []),
+        "youth_icp_device_count": (c_int, []),
+        "youth_icp_align_batch": (c_int, [P16, P16, c_int, c_int, c_int, POINTER(Intrinsics),
+                                          c_int, PF, PI32]),
+        "youth_icp_create": (c_void_p, [c_int, c_int, c_int, c_int, POINTER(Intrinsics),
+                                        POINTER(Params)]),
+        "youth_icp_destroy": (None, [c_void_p]),
+        "youth_icp_align_pairs_device": (c_int, [c_void_p, c_void_p, c_void_p, c_int, PD,
+                                                 c_void_p, c_void_p]),
+        "youth_icp_align_sequence_device": (c_int, [c_void_p, c_void_p, c_int, c_void_p,
+                                                    c_void_p]),
+        "youth_icp_sync": (c_int, [c_void_p, c_void_p]),
+        "youth_icp_get_poses": (c_int, [c_void_p, c_int, PD, PF, PI32]),
+        "youth_icp_get_stats": (c_int, [c_void_p, c_int, c_int, PD, PD]),
+        "youth_icp_set_timing": (c_int, [c_void_p, c_int]),
+        "youth_icp_get_timing": (c_int, [c_void_p, c_int, PD, POINTER(c_int)]),
+        "youth_icp_prepare_host": (c_int, [c_void_p, P16, c_int, c_int, PF, PF, PF, PF, PF,
+                                           PF]),
+        "youth_icp_reduce_host": (c_int, [c_void_p, P16, P16, PF, PI32, PD]),
+        "youth_icp_solve_host": (c_int, [c_void_p, PD, PD]),
+        "youth_icp_track_frame": (c_int, [c_void_p, P16, PD, PD, POINTER(c_int)]),
+        "youth_icp_track_reset": (None, [c_void_p]),
+        "youth_parse_camera_yaml": (c_int, [c_char_p, POINTER(Intrinsics), POINTER(c_int),
+                                            POINTER(c_int)]),
+        "youth_queue_create": (c_void_p, [c_int, c_int]),
+        "youth_queue_destroy": (None, [c_void_p]),
+        "youth_queue_push": (c_int, [c_void_p, P16, c_int, c_int, c_uint32]),
+        "youth_queue_pop": (c_int, [c_void_p, P16, c_size_t, POINTER(c_int), POINTER(c_int),
+                                    POINTER(c_uint32)]),
+        "youth_queue_size": (c_int, [c_void_p]),
+        "youth_queue_clear": (None, [c_void_p]),
+        "youth_slam_trajectory_length": (c_int, []),
+        "youth_slam_get_trajectory": (c_int, [c_int, POINTER(c_uint32), PD]),
+        "youth_slam_wait_idle": (c_int, [c_int]),
+        "youth_slam_wait_stopped": (None, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def declared_functions(header: str = HEADER_PATH) -> list[str]:
+    """Function names declared in include/youth_icp.h (for the ABI test)."""
+    text = open(header).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"\b([A-Za-z_]\w*)\s*\([^;{]*\)\s*;", text)
+    return sorted({n for n in names if n not in ("sizeof",)})
+
+
+def _p(arr, ctype):
+    return None if arr is None else arr.ctypes.data_as(POINTER(ctype))
+
+
+def _err(code: int) -> IcpError:
+    lib = load_library()
+    return IcpError(code, (lib.youth_icp_last_error() or b"").decode())
+
+
+def _check(code: int) -> int:
+    if code < 0:
+        raise _err(code)
+    return code
+
+
+def default_intrinsics(width: int, height: int) -> Intrinsics:
+    return load_library().youth_default_intrinsics(width, height)
+
+
+def default_params() -> Params:
+    return load_library().youth_default_params()
+
+
+def device_count() -> int:
+    return load_library().youth_icp_device_count()
+
+
+# ----------------------------------------------------------- SLAM.h mirror --
+def initSlamModule(config_file: str | None, vocabulary_file: str | None = None) -> None:
+    load_library().initSlamModule(config_file.encode() if config_file else None,
+                                  vocabulary_file.encode() if vocabulary_file else None)
+
+
+def stopSlamModule() -> None:
+    load_library().stopSlamModule()
+
+
+def processSlamFrame(depth_data: np.ndarray, color_data: np.ndarray | None, width: int,
+                     height: int, timestamp: int) -> int:
+    depth = np.ascontiguousarray(depth_data, dtype=np.int16)
+    if depth.size < width * height:
+        return 0
+    color = None if color_data is None else np.ascontiguousarray(color_data, dtype=np.uint8)
+    return load_library().processSlamFrame(_p(depth, c_int16), _p(color, c_uint8), width,
+                                           height, timestamp)
+
+
+def saveSlamMap(map_file: str) -> int:
+    return load_library().saveSlamMap(map_file.encode())
+
+
+def isSlamModuleRunning() -> int:
+    return load_library().isSlamModuleRunning()
+
+
+def getSlamMapPoints() -> int:
+    return load_library().getSlamMapPoints()
+
+
+def resetSlam() -> None:
+    load_library().resetSlam()
+
+
+def slam_wait_idle(timeout_ms: int = 10000) -> int:
+    return load_library().youth_slam_wait_idle(timeout_ms)
+
+
+def slam_trajectory() -> tuple[np.ndarray, np.ndarray]:
+    lib = load_library()
+    n = lib.youth_slam_trajectory_length()
+    ts = np.zeros(n, np.uint32)
+    T = np.zeros((n, 4, 4), np.float64)
+    m = lib.youth_slam_get_trajectory(n, _p(ts, c_uint32), _p(T, c_double))
+    return ts[:m], T[:m]
+
+
+def parse_camera_yaml(path: str, width: int = 640, height: int = 480):
+    """(Intrinsics, W, H) from an ORB-SLAM3-style YAML; None if unreadable."""
+    lib = load_library()
+    K = lib.youth_default_intrinsics(width, height)
+    W, H = c_int(0), c_int(0)
+    ok = lib.youth_parse_camera_yaml(path.encode(), ctypes.byref(K), ctypes.byref(W),
+                                     ctypes.byref(H))
+    return (K, W.value, H.value) if ok else None
+
+
+# ---------------------------------------------------------- ingest queue --
+class FrameQueue:
+    """The bounded ingest queue (SLAM.cpp:159-169 policy)."""
+
+    def __init__(self, high_water: int = 10, low_water: int = 5):
+        self._lib = load_library()
+        self._q = self._lib.youth_queue_create(high_water, low_water)
+        if not self._q:
+            raise IcpError(YOUTH_EINVAL, "bad queue watermarks")
+
+    def push(self, depth: np.ndarray, timestamp: int = 0) -> int:
+        d = np.ascontiguousarray(depth, dtype=np.int16)
+        return _check(self._lib.youth_queue_push(self._q, _p(d, c_int16), d.shape[1],
+                                                 d.shape[0], timestamp))
+
+    def pop(self, cap: int = 4096 * 4096):
+        buf = np.empty(cap, np.int16)
+        w, h, ts = c_int(0), c_int(0), c_uint32(0)
+        rc = _check(self._lib.youth_queue_pop(self._q, _p(buf, c_int16), cap, ctypes.byref(w),
+                                              ctypes.byref(h), ctypes.byref(ts)))
+        if rc == 0:
+            return None
+        return buf[: w.value * h.value].reshape(h.value, w.value).copy(), ts.value
+
+    def __len__(self):
+        return self._lib.youth_queue_size(self._q)
+
+    def clear(self):
+        self._lib.youth_queue_clear(self._q)
+
+    def close(self):
+        if self._q:
+            self._lib.youth_queue_destroy(self._q)
+            self._q = None
+
+    __del__ = close
+
+
+# -------------------------------------------------------- additive API --
+class IcpContext:
+    """Device workspace for W x H frames (youth_icp_create)."""
+
+    def __init__(self, width: int, height: int, max_frames: int, K: Intrinsics | None = None,
+                 iters: int = 10, dist_thresh: float = 0.10, device: int = 0):
+        self._lib = load_library()
+        self.W, self.H, self.max_frames = width, height, max_frames
+        self.K = K if K is not None else default_intrinsics(width, height)
+        self.params = Params(iters, dist_thresh)
+        self._ctx = self._lib.youth_icp_create(device, width, height, max_frames,
+                                               ctypes.byref(self.K), ctypes.byref(self.params))
+        if not self._ctx:
+            msg = (self._lib.youth_icp_last_error() or b"").decode()
+            raise IcpError(YOUTH_ENODEV if "no HIP device" in msg else YOUTH_EHIP, msg)
+
+    @property
+    def handle(self) -> int:
+        return self._ctx
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self._lib.youth_icp_destroy(self._ctx)
+            self._ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        self.close()
+
+    # device-pointer API (pointers as ints, e.g. torch tensor.data_ptr())
+    def align_pairs_device(self, d_src: int, d_dst: int, n_pairs: int, T_init=None,
+                           d_T_out: int = 0, stream: int = 0) -> None:
+        Ti = None if T_init is None else np.ascontiguousarray(T_init, np.float64)
+        _check(self._lib.youth_icp_align_pairs_device(self._ctx, d_src, d_dst, n_pairs,
+                                                      _p(Ti, c_double), d_T_out or None,
+                                                      stream or None))
+
+    def align_sequence_device(self, d_frames: int, n_frames: int, d_T_out: int = 0,
+                              stream: int = 0) -> None:
+        _check(self._lib.youth_icp_align_sequence_device(self._ctx, d_frames, n_frames,
+                                                         d_T_out or None, stream or None))
+
+    def sync(self, stream: int = 0) -> None:
+        _check(self._lib.youth_icp_sync(self._ctx, stream or None))
+
+    def get_poses(self, n: int):
+        T64 = np.zeros((n, 4, 4), np.float64)
+        T32 = np.zeros((n, 4, 4), np.float32)
+        st = np.zeros(n, np.int32)
+        _check(self._lib.youth_icp_get_poses(self._ctx, n, _p(T64, c_double), _p(T32, c_float),
+                                             _p(st, c_int32)))
+        T64[:, 3, :] = (0.0, 0.0, 0.0, 1.0)
+        return T64, T32, st
+
+    def get_stats(self, n: int, iters: int):
+        cnt = np.zeros((n, iters), np.float64)
+        r2 = np.zeros((n, iters), np.float64)
+        _check(self._lib.youth_icp_get_stats(self._ctx, n, iters, _p(cnt, c_double),
+                                             _p(r2, c_double)))
+        return cnt, r2
+
+    def set_timing(self, enable: bool) -> None:
+        _check(self._lib.youth_icp_set_timing(self._ctx, 1 if enable else 0))
+
+    def get_timing(self, kind: int = 0):
+        ms, n = c_double(0.0), c_int(0)
+        _check(self._lib.youth_icp_get_timing(self._ctx, kind, ctypes.byref(ms),
+                                              ctypes.byref(n)))
+        return ms.value, n.value
+
+    # host-array stage entry points (parity tests)
+    def prepare(self, depth: np.ndarray, want_normals: bool = True):
+        d = np.ascontiguousarray(depth, np.int16).reshape(-1, self.H, self.W)
+        n = d.shape[0]
+        outs = [np.zeros((n, self.H, self.W), np.float32) for _ in range(6)]
+        _check(self._lib.youth_icp_prepare_host(self._ctx, _p(d, c_int16), n,
+                                                1 if want_normals else 0,
+                                                *[_p(o, c_float) for o in outs]))
+        return outs
+
+    def reduce(self, src: np.ndarray, dst: np.ndarray, T12: np.ndarray, want_assoc=True):
+        s = np.ascontiguousarray(src, np.int16)
+        d = np.ascontiguousarray(dst, np.int16)
+        T = np.ascontiguousarray(np.asarray(T12, np.float32).reshape(-1)[:12])
+        assoc = np.zeros(self.W * self.H, np.int32) if want_assoc else None
+        neq = np.zeros(YOUTH_NEQ, np.float64)
+        _check(self._lib.youth_icp_reduce_host(self._ctx, _p(s, c_int16), _p(d, c_int16),
+                                               _p(T, c_float), _p(assoc, c_int32),
+                                               _p(neq, c_double)))
+        return assoc, neq
+
+    def solve(self, neq: np.ndarray, T64: np.ndarray):
+        nq = np.ascontiguousarray(neq, np.float64)
+        T = np.ascontiguousarray(np.array(T64, np.float64).reshape(4, 4))
+        st = _check(self._lib.youth_icp_solve_host(self._ctx, _p(nq, c_double),
+                                                   _p(T, c_double)))
+        return T, st
+
+    def track_frame(self, depth: np.ndarray, T_init=None):
+        d = np.ascontiguousarray(depth, np.int16)
+        Ti = None if T_init is None else np.ascontiguousarray(T_init, np.float64)
+        T = np.zeros((4, 4), np.float64)
+        has = c_int(0)
+        st = _check(self._lib.youth_icp_track_frame(self._ctx, _p(d, c_int16), _p(Ti, c_double),
+                                                    _p(T, c_double), ctypes.byref(has)))
+        return T, st, bool(has.value)
+
+    def track_reset(self) -> None:
+        self._lib.youth_icp_track_reset(self._ctx)
+
+
+def align_batch(src: np.ndarray, dst: np.ndarray, K: Intrinsics | None = None, iters: int = 10,
+                want_assoc: bool = False):
+    """youth_icp_align_batch: src/dst [n, H, W] int16 -> (T [n,4,4] fp32, assoc|None)."""
+    s = np.ascontiguousarray(src, np.int16)
+    d = np.ascontiguousarray(dst, np.int16)
+    if s.ndim == 2:
+        s, d = s[None], d[None]
+    n, H, W = s.shape
+    T = np.zeros((n, 4, 4), np.float32)
+    assoc = np.zeros((n, H * W), np.int32) if want_assoc else None
+    lib = load_library()
+    Kp = ctypes.byref(K) if K is not None else None
+    _check(lib.youth_icp_align_batch(_p(s, c_int16), _p(d, c_int16), n, W, H, Kp, iters,
+                                     _p(T, c_float), _p(assoc, c_int32)))
+    return T, assoc

@@ -1,0 +1,99 @@
+"""Generate the committed golden fixtures (tests/golden/*.npz).
+
+Run from the repo root:  python tests/golden/make_golden.py
+
+Provenance, case by case:
+  * kat_backproject — the back-projection known-answer table of SURVEY.md §4,
+    computed by the survey from the reference formula viewerModule.c:343-345
+    with gcc -O2 -ffp-contract=off (x86-64 SSE fp32).  These are the only
+    vectors pinned to the REFERENCE; they are written out here verbatim.
+  * pair_* / seq_* — inputs from the synthetic depth source
+    (libyouth_synth.so), expected outputs from the C oracle
+    (oracle/liboracle.so).  The reference has no ICP, so
+    these pin this build's own spec against regressions: "parity unpinned"
+    with respect to the reference beyond back-projection.
+
+Fixtures are data only (numpy .npz, loaded with allow_pickle=False).
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "slam-rgbd_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import oracle  # noqa: E402
+import youth_synth  # noqa: E402
+
+# (W, H, u, v, d_mm, X_bits, Y_bits, Z_bits)
+KAT = [
+    (640, 480, 0, 0, 1000, 0xBF0FA4C9, 0xBED7772E, 0x3F800000),
+    (640, 480, 639, 479, 4000, 0x400F31DF, 0x3FD6915A, 0x40800000),
+    (640, 480, 320, 240, 1234, 0x00000000, 0x00000000, 0x3F9DF3B6),
+    (640, 480, 17, 401, 32767, 0xC18B45CE, 0x41140186, 0x42031168),
+    (1280, 960, 1279, 0, 2500, 0x40334629, 0xC006AA7D, 0x40200000),
+]
+
+
+def scaled_K(W, H):
+    """Focal length scaled with the width so small frames keep a 58 deg FOV."""
+    return oracle.OracleIntrinsics(570.3 * W / 640.0, 570.3 * W / 640.0, float(W // 2),
+                                   float(H // 2), 1000.0)
+
+
+def make_pair_case(name, W, H, index, iters=10, dist=0.10):
+    K = scaled_K(W, H)
+    src, dst, Tgt = youth_synth.pairs(index, 1, W, H, K=_yk(K))
+    src, dst = src[0], dst[0]
+    sX, sY, sZ = oracle.backproject(src, K)
+    tX, tY, tZ = oracle.backproject(dst, K)
+    nX, nY, nZ = oracle.normals(tX, tY, tZ)
+    I12 = np.eye(4, dtype=np.float32)[:3]
+    idx0 = oracle.associate(src, dst, I12, K, dist)
+    neq0 = oracle.reduce(src, dst, I12, K, dist)
+    T64, T32, st, stats = oracle.align(src, dst, K, iters, dist)
+    idxF = oracle.associate(src, dst, T32, K, dist)
+    np.savez_compressed(
+        os.path.join(HERE, name + ".npz"), src=src, dst=dst,
+        K=np.array([K.fx, K.fy, K.cx, K.cy, K.depth_scale], np.float32),
+        iters=np.int32(iters), dist_thresh=np.float32(dist), T_gt=Tgt[0],
+        src_xyz=np.stack([sX, sY, sZ]), dst_xyz=np.stack([tX, tY, tZ]),
+        dst_nrm=np.stack([nX, nY, nZ]), idx_identity=idx0, neq_identity=neq0,
+        T64=T64, T32=T32, status=np.int32(st), stats=stats, idx_final=idxF)
+    print(f"{name}: status={st} matches0={int((idx0 >= 0).sum())} "
+          f"final count={stats[-1, 0]:.0f}")
+
+
+def _yk(K):
+    from youth_icp import Intrinsics
+    return Intrinsics(K.fx, K.fy, K.cx, K.cy, K.depth_scale)
+
+
+def make_seq_case(name, W, H, n_frames, iters=10, dist=0.10):
+    K = scaled_K(W, H)
+    frames, Twc = youth_synth.sequence(0, n_frames, W, H, K=_yk(K))
+    rel = []
+    for k in range(n_frames - 1):
+        T64, T32, st, _ = oracle.align(frames[k + 1], frames[k], K, iters, dist)
+        rel.append(T64)
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), frames=frames,
+                        K=np.array([K.fx, K.fy, K.cx, K.cy, K.depth_scale], np.float32),
+                        iters=np.int32(iters), dist_thresh=np.float32(dist), T_wc=Twc,
+                        T_rel=np.stack(rel))
+    print(f"{name}: {n_frames} frames")
+
+
+def main():
+    np.savez_compressed(os.path.join(HERE, "kat_backproject.npz"),
+                        table=np.array(KAT, dtype=np.int64))
+    make_pair_case("pair_80x60", 80, 60, 0)
+    make_pair_case("pair_160x120", 160, 120, 1)
+    make_pair_case("pair_97x53", 97, 53, 2)
+    make_seq_case("seq_128x96", 128, 96, 6)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,142 @@
+"""CPU tests of the C-ABI boundary: the library loads, exports every function
+include/*.h declares, and the host-only logic (queue policy, YAML intrinsics,
+no-device behaviour, synthetic source) behaves as the reference's API says.
+No compute calls here."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import youth_icp
+import youth_synth
+from conftest import GOLDEN, PKG, ROOT
+
+HEADERS = {
+    "youth_icp.h": os.path.join(PKG, "libyouth_icp.so"),
+    "youth_synth.h": os.path.join(PKG, "libyouth_synth.so"),
+}
+
+
+def _exported(lib_path):
+    out = subprocess.run(["nm", "-D", "--defined-only", lib_path], capture_output=True,
+                         text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+@pytest.mark.parametrize("header", sorted(HEADERS))
+def test_every_declared_symbol_is_exported(header):
+    names = youth_icp.declared_functions(os.path.join(ROOT, "include", header))
+    assert len(names) >= (35 if header == "youth_icp.h" else 4)
+    exported = _exported(HEADERS[header])
+    missing = [n for n in names if n not in exported]
+    assert not missing, missing
+    lib = ctypes.CDLL(HEADERS[header])
+    for n in names:
+        getattr(lib, n)
+
+
+def test_reference_api_names_present():
+    """SLAM.h:11-38 + algorithmModule.h:6, exactly these names."""
+    ref = ["initSlamModule", "stopSlamModule", "processSlamFrame", "saveSlamMap",
+           "isSlamModuleRunning", "getSlamMapPoints", "resetSlam", "algorithmModule"]
+    assert set(ref) <= _exported(HEADERS["youth_icp.h"])
+
+
+def test_header_compiles_as_c99_and_cpp():
+    src = '#include "youth_icp.h"\n#include "youth_synth.h"\nint main(void){return 0;}\n'
+    inc = os.path.join(ROOT, "include")
+    for cc, std in (("gcc", "-std=c99"), ("g++", "-std=c++11")):
+        r = subprocess.run([cc, std, "-Wall", "-Werror", "-fsyntax-only", "-I", inc, "-x",
+                            "c" if cc == "gcc" else "c++", "-"], input=src, text=True,
+                           capture_output=True)
+        assert r.returncode == 0, r.stderr
+
+
+def test_default_intrinsics_follow_viewer_convention():
+    K = youth_icp.default_intrinsics(640, 480)
+    assert K.as_tuple() == (np.float32(570.3), np.float32(570.3), 320.0, 240.0, 1000.0)
+    K = youth_icp.default_intrinsics(1281, 961)
+    assert (K.cx, K.cy) == (640.0, 480.0)           # integer W/2 (viewerModule.c:344)
+    P = youth_icp.default_params()
+    assert P.iters == 10 and abs(P.dist_thresh - 0.1) < 1e-7
+
+
+def test_no_device_fails_loudly(has_gpu):
+    if has_gpu:
+        pytest.skip("only meaningful without a GPU")
+    assert youth_icp.device_count() == 0
+    with pytest.raises(youth_icp.IcpError) as e:
+        youth_icp.IcpContext(64, 48, 2)
+    assert e.value.code == youth_icp.YOUTH_ENODEV
+    src = np.ones((1, 48, 64), np.int16)
+    with pytest.raises(youth_icp.IcpError):
+        youth_icp.align_batch(src, src)
+    # SLAM.h API: the module refuses to start, so frames are rejected (return 0)
+    youth_icp.initSlamModule(None)
+    assert youth_icp.isSlamModuleRunning() == 0
+    assert youth_icp.processSlamFrame(src[0], None, 64, 48, 0) == 0
+    assert youth_icp.saveSlamMap("/tmp/youth_nomap") == 0
+    assert youth_icp.getSlamMapPoints() == 0
+    lib = youth_icp.load_library()
+    assert lib.algorithmModule(None) is None     # returns instead of hanging
+
+
+def test_queue_overflow_policy_matches_reference():
+    """SLAM.cpp:159-169: push, then if size > 10 drop oldest until size == 5."""
+    q = youth_icp.FrameQueue(10, 5)
+    frames = [np.full((4, 6), i, np.int16) for i in range(12)]
+    dropped = [q.push(f, timestamp=100 + i) for i, f in enumerate(frames)]
+    assert dropped[:10] == [0] * 10 and dropped[10] == 6 and dropped[11] == 0
+    assert len(q) == 6
+    out = [q.pop() for _ in range(6)]
+    assert [ts for _, ts in out] == [106, 107, 108, 109, 110, 111]
+    assert all((d == ts - 100).all() and d.shape == (4, 6) for d, ts in out)
+    assert q.pop() is None and len(q) == 0
+    q.push(frames[0])
+    q.clear()
+    assert len(q) == 0
+    q.close()
+
+
+def test_queue_copies_frames():
+    q = youth_icp.FrameQueue()
+    f = np.arange(12, dtype=np.int16).reshape(3, 4)
+    q.push(f, 1)
+    f[:] = -1                                   # caller reuses its buffer immediately
+    d, ts = q.pop()
+    assert (d == np.arange(12).reshape(3, 4)).all() and ts == 1
+
+
+def test_parse_camera_yaml():
+    K, W, H = youth_icp.parse_camera_yaml(os.path.join(GOLDEN, "astra_camera.yaml"))
+    assert (K.fx, K.fy, K.cx, K.cy, K.depth_scale) == (np.float32(570.3), np.float32(570.3),
+                                                       320.0, 240.0, 1000.0)
+    assert (W, H) == (640, 480)
+    assert youth_icp.parse_camera_yaml("/nonexistent.yaml") is None
+
+
+def test_synth_deterministic_and_valid():
+    a = youth_synth.pairs(0, 2, 160, 120)
+    b = youth_synth.pairs(0, 2, 160, 120)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    src, dst, T = a
+    valid = src[src > 0]
+    assert 400 <= valid.min() and valid.max() <= 8000
+    assert 0.95 < (src > 0).mean() < 0.995          # ~2 % holes
+    R = T[:, :3, :3]
+    assert np.allclose(R @ R.transpose(0, 2, 1), np.eye(3), atol=1e-12)
+    ang = np.degrees(np.arccos(np.clip((np.trace(R, axis1=1, axis2=2) - 1) / 2, -1, 1)))
+    assert (ang <= 1.5 + 1e-9).all() and (np.abs(T[:, :3, 3]) <= 0.015).all()
+    g = np.load(os.path.join(GOLDEN, "pair_160x120.npz"), allow_pickle=False)
+    K = youth_icp.Intrinsics(*[float(v) for v in g["K"]])
+    s2, d2, _ = youth_synth.pairs(1, 1, 160, 120, K=K)
+    assert np.array_equal(s2[0], g["src"]) and np.array_equal(d2[0], g["dst"])
+
+
+def test_synth_sequence_shards_consistent():
+    full, T = youth_synth.sequence(0, 6, 64, 48)
+    part, T2 = youth_synth.sequence(3, 3, 64, 48)
+    assert np.array_equal(full[3:], part) and np.array_equal(T[3:], T2)

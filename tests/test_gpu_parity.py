@@ -1,0 +1,303 @@
+"""GPU parity tests: the HIP path (through the C-ABI) against the C oracle.
+
+Bar:
+  * XYZ, normals, association indices: bit-exact (given the same fp32 pose);
+  * normal-equation sums: fp64, differ only by summation order -> rel 1e-12;
+  * recovered SE(3) pose: max |T_gpu - T_cpu| over the 3x4 entries <= 1e-5
+    (north_star tolerance; observed ~1e-15).
+"""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+import oracle
+import youth_icp
+import youth_synth
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+POSE_TOL = 1e-5
+
+
+def _load(name):
+    return np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+
+
+def _K(arr):
+    return youth_icp.Intrinsics(*[float(v) for v in arr])
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def _pose_err(A, B):
+    return float(np.abs(np.asarray(A)[:3, :4] - np.asarray(B)[:3, :4]).max())
+
+
+# --------------------------------------------------------------- prepare --
+def test_backproject_kat_on_gpu():
+    table = _load("kat_backproject")["table"].tolist()
+    for W, H in {(r[0], r[1]) for r in table}:
+        depth = np.zeros((H, W), np.int16)
+        rows = [r for r in table if (r[0], r[1]) == (W, H)]
+        for _, _, u, v, d, *_ in rows:
+            depth[v, u] = d
+        with youth_icp.IcpContext(W, H, 2) as ctx:
+            X, Y, Z, *_ = ctx.prepare(depth, want_normals=False)
+        for _, _, u, v, d, xb, yb, zb in rows:
+            got = (int(_bits(X[0, v, u])), int(_bits(Y[0, v, u])), int(_bits(Z[0, v, u])))
+            assert got == (xb, yb, zb), (W, H, u, v, d)
+
+
+@pytest.mark.parametrize("W,H", [(640, 480), (97, 53), (64, 16), (1280, 960), (65, 17)])
+def test_prepare_bit_exact(W, H):
+    src, dst, _ = youth_synth.pairs(11, 2, W, H)
+    frames = np.concatenate([src, dst])
+    # exercise invalid / extreme raw values too
+    frames[0, 0, :5] = [-1, -32768, 32767, 0, 1]
+    with youth_icp.IcpContext(W, H, 4) as ctx:
+        X, Y, Z, NX, NY, NZ = ctx.prepare(frames, want_normals=True)
+    for f in range(4):
+        oX, oY, oZ = oracle.backproject(frames[f])
+        oN = oracle.normals(oX, oY, oZ)
+        assert np.array_equal(_bits(X[f]), _bits(oX))
+        assert np.array_equal(_bits(Y[f]), _bits(oY))
+        assert np.array_equal(_bits(Z[f]), _bits(oZ))
+        for g, o in zip((NX[f], NY[f], NZ[f]), oN):
+            assert np.array_equal(_bits(g), _bits(o)), f
+
+
+@pytest.mark.parametrize("name", ["pair_80x60", "pair_160x120", "pair_97x53"])
+def test_prepare_matches_golden(name):
+    g = _load(name)
+    K = _K(g["K"])
+    H, W = g["src"].shape
+    with youth_icp.IcpContext(W, H, 2, K=K) as ctx:
+        out = ctx.prepare(np.stack([g["src"], g["dst"]]), want_normals=True)
+    assert np.array_equal(_bits(np.stack(out[:3])[:, 0]), _bits(g["src_xyz"]))
+    assert np.array_equal(_bits(np.stack(out[:3])[:, 1]), _bits(g["dst_xyz"]))
+    assert np.array_equal(_bits(np.stack(out[3:])[:, 1]), _bits(g["dst_nrm"]))
+
+
+# ---------------------------------------------------------- association --
+@pytest.mark.parametrize("name", ["pair_80x60", "pair_160x120", "pair_97x53"])
+def test_assoc_and_reduce_match_golden(name):
+    g = _load(name)
+    K = _K(g["K"])
+    H, W = g["src"].shape
+    with youth_icp.IcpContext(W, H, 2, K=K, dist_thresh=float(g["dist_thresh"])) as ctx:
+        I12 = np.eye(4, dtype=np.float32)[:3]
+        assoc, neq = ctx.reduce(g["src"], g["dst"], I12)
+        assert np.array_equal(assoc, g["idx_identity"])
+        np.testing.assert_allclose(neq, g["neq_identity"], rtol=1e-12, atol=1e-12)
+        assoc, _ = ctx.reduce(g["src"], g["dst"], g["T32"])
+        assert np.array_equal(assoc, g["idx_final"])
+
+
+def test_assoc_bit_exact_every_iteration_640x480():
+    """Index bit-exactness given the SAME fp32 pose: feed the oracle's T_k."""
+    src, dst, _ = youth_synth.pairs(0, 1)
+    src, dst = src[0], dst[0]
+    K = oracle.viewer_K(640, 480)
+    with youth_icp.IcpContext(640, 480, 2) as ctx:
+        T = np.eye(4)
+        for it in range(10):
+            T32 = T[:3].astype(np.float32)
+            g_idx, g_neq = ctx.reduce(src, dst, T32)
+            o_idx = oracle.associate(src, dst, T32, K)
+            o_neq = oracle.reduce(src, dst, T32, K)
+            assert np.array_equal(g_idx, o_idx), it
+            np.testing.assert_allclose(g_neq, o_neq, rtol=1e-11, atol=1e-9)
+            xi, st = oracle.solve(o_neq)
+            assert st == 0
+            T = oracle.se3_exp(xi) @ T
+
+
+def test_solve_matches_oracle():
+    src, dst, _ = youth_synth.pairs(5, 1, 320, 240)
+    K = oracle.viewer_K(320, 240)
+    neq = oracle.reduce(src[0], dst[0], np.eye(4, dtype=np.float32)[:3], K)
+    xi, st = oracle.solve(neq)
+    T0 = np.eye(4)
+    T0[:3, 3] = [0.01, -0.02, 0.03]
+    with youth_icp.IcpContext(320, 240, 2) as ctx:
+        Tg, stg = ctx.solve(neq, T0)
+        assert stg == st == 0
+        assert np.abs(Tg - oracle.se3_exp(xi) @ T0).max() < 1e-13
+        bad = np.zeros(29)
+        bad[28] = 3
+        Tb, stb = ctx.solve(bad, T0)
+        assert stb == youth_icp.STATUS_FEW_MATCHES and np.array_equal(Tb, T0)
+        bad[28] = 100
+        Tb, stb = ctx.solve(bad, T0)
+        assert stb == youth_icp.STATUS_DEGENERATE and np.array_equal(Tb, T0)
+
+
+# ----------------------------------------------------------- full align --
+def test_align_batch_640x480_matches_oracle():
+    n = 8
+    src, dst, Tgt = youth_synth.pairs(0, n)
+    Tg, assoc = youth_icp.align_batch(src, dst, iters=10, want_assoc=True)
+    for p in range(n):
+        T64, T32, st, _ = oracle.align(src[p], dst[p], iters=10)
+        assert st == 0
+        assert _pose_err(Tg[p], T64) <= POSE_TOL, p
+        assert np.array_equal(assoc[p], oracle.associate(src[p], dst[p], Tg[p][:3]))
+
+
+def test_context_device_api_poses_and_stats():
+    n = 6
+    src, dst, _ = youth_synth.pairs(20, n)
+    import ctypes
+    with youth_icp.IcpContext(640, 480, 2 * n) as ctx:
+        # host arrays through the one-shot path, then the context getters
+        Tb, _ = youth_icp.align_batch(src, dst, iters=10)
+        T_init = np.tile(np.eye(4), (n, 1, 1))
+        lib = youth_icp.load_library()
+        # device copies via the library's own stream: use align_batch's staging
+        hs = np.ascontiguousarray(src)
+        hd = np.ascontiguousarray(dst)
+        import torch  # plumbing only: device memory
+        ds = torch.from_numpy(hs).cuda()
+        dd = torch.from_numpy(hd).cuda()
+        out = torch.zeros((n, 16), dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), n, T_init=T_init,
+                               d_T_out=out.data_ptr())
+        ctx.sync()
+        T64, T32, st = ctx.get_poses(n)
+        cnt, r2 = ctx.get_stats(n, 10)
+        Tdev = out.cpu().numpy().reshape(n, 4, 4)
+        del lib, ctypes
+    for p in range(n):
+        T64o, _, sto, stats = oracle.align(src[p], dst[p], iters=10)
+        assert _pose_err(T64[p], T64o) <= POSE_TOL
+        assert np.array_equal(Tdev[p], T32[p]) and np.array_equal(Tdev[p], Tb[p])
+        assert st[p] == sto
+        assert np.array_equal(cnt[p], stats[:, 0])
+        np.testing.assert_allclose(r2[p], stats[:, 1], rtol=1e-9)
+
+
+def test_align_1280x960_20_iters():
+    src, dst, _ = youth_synth.pairs(3, 2, 1280, 960)
+    K = youth_icp.default_intrinsics(1280, 960)
+    Tg, _ = youth_icp.align_batch(src, dst, K=K, iters=20)
+    for p in range(2):
+        T64, _, st, _ = oracle.align(src[p], dst[p], iters=20)
+        assert st == 0 and _pose_err(Tg[p], T64) <= POSE_TOL
+
+
+@pytest.mark.parametrize("name", ["pair_80x60", "pair_160x120", "pair_97x53"])
+def test_align_matches_golden_pose(name):
+    g = _load(name)
+    Tg, _ = youth_icp.align_batch(g["src"][None], g["dst"][None], K=_K(g["K"]),
+                                  iters=int(g["iters"]))
+    assert _pose_err(Tg[0], g["T64"]) <= POSE_TOL
+
+
+def test_identity_and_empty_edge_cases():
+    src, dst, _ = youth_synth.pairs(9, 1, 160, 120)
+    z = np.zeros((160 * 120,), np.int16).reshape(120, 160)
+    S = np.stack([dst[0], z, z, dst[0]])
+    D = np.stack([dst[0], z, dst[0], z])
+    with youth_icp.IcpContext(160, 120, 8, iters=3) as ctx:
+        import torch
+        ds = torch.from_numpy(S).cuda()
+        dd = torch.from_numpy(D).cuda()
+        torch.cuda.synchronize()
+        ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), 4)
+        T64, _, st = ctx.get_poses(4)
+    assert np.array_equal(T64[0], np.eye(4)) and st[0] == 0       # identical frames
+    for p in (1, 2, 3):                                             # empty source/target
+        assert np.array_equal(T64[p], np.eye(4)) and st[p] == youth_icp.STATUS_FEW_MATCHES
+
+
+def test_sequence_api_matches_oracle():
+    g = _load("seq_128x96")
+    frames = g["frames"]
+    n = frames.shape[0]
+    import torch
+    with youth_icp.IcpContext(128, 96, n, K=_K(g["K"]), iters=int(g["iters"])) as ctx:
+        d = torch.from_numpy(frames).cuda()
+        torch.cuda.synchronize()
+        ctx.align_sequence_device(d.data_ptr(), n)
+        T64, _, st = ctx.get_poses(n - 1)
+    for k in range(n - 1):
+        assert _pose_err(T64[k], g["T_rel"][k]) <= POSE_TOL, k
+
+
+def test_track_frame_matches_oracle():
+    frames, _ = youth_synth.sequence(0, 5)
+    with youth_icp.IcpContext(640, 480, 2) as ctx:
+        T, st, has = ctx.track_frame(frames[0])
+        assert not has and np.array_equal(T, np.eye(4))
+        for k in range(1, 5):
+            T, st, has = ctx.track_frame(frames[k])
+            T64, _, sto, _ = oracle.align(frames[k], frames[k - 1])
+            assert has and st == sto and _pose_err(T, T64) <= POSE_TOL
+        ctx.track_reset()
+        T, st, has = ctx.track_frame(frames[4])
+        assert not has
+
+
+# ------------------------------------------------------- SLAM.h drop-in --
+def test_slam_api_end_to_end():
+    frames, Twc = youth_synth.sequence(0, 8)
+    cfg = os.path.join(GOLDEN, "astra_camera.yaml")
+    youth_icp.initSlamModule(cfg, "ORBvoc.txt")
+    try:
+        assert youth_icp.isSlamModuleRunning() == 1
+        for k in range(8):
+            assert youth_icp.processSlamFrame(frames[k], None, 640, 480, 1000 + 33 * k) == 1
+            assert youth_icp.slam_wait_idle(20000) == 1      # keep the queue from dropping
+        ts, T = youth_icp.slam_trajectory()
+        assert list(ts) == [1000 + 33 * k for k in range(8)]
+        assert youth_icp.getSlamMapPoints() == int((frames[7] > 0).sum())
+        # world poses = prefix product of the oracle's relative poses
+        acc = np.eye(4)
+        assert np.array_equal(T[0], acc)
+        for k in range(1, 8):
+            T64, _, _, _ = oracle.align(frames[k], frames[k - 1])
+            acc = acc @ T64
+            assert _pose_err(T[k], acc) <= POSE_TOL
+        with tempfile.TemporaryDirectory() as td:
+            base = os.path.join(td, "map")
+            assert youth_icp.saveSlamMap(base) == 1
+            rows = np.loadtxt(base + "_trajectory.txt")
+            assert rows.shape == (8, 8) and os.path.exists(base + "_keyframes.txt")
+            assert np.allclose(rows[:, 0], ts)
+            assert np.allclose(rows[:, 1:4], T[:, :3, 3], atol=1e-8)
+            assert np.allclose(np.linalg.norm(rows[:, 4:], axis=1), 1.0)
+        youth_icp.resetSlam()
+        assert youth_icp.processSlamFrame(frames[0], None, 640, 480, 5) == 1
+        assert youth_icp.slam_wait_idle(20000) == 1
+        ts, T = youth_icp.slam_trajectory()
+        assert list(ts) == [5] and np.array_equal(T[0], np.eye(4))
+    finally:
+        youth_icp.stopSlamModule()
+    assert youth_icp.isSlamModuleRunning() == 0
+    assert youth_icp.processSlamFrame(frames[0], None, 640, 480, 0) == 0
+
+
+def test_algorithm_module_thread_entry():
+    import threading
+    lib = youth_icp.load_library()
+    t = threading.Thread(target=lambda: lib.algorithmModule(None))
+    t.start()
+    for _ in range(200):
+        if youth_icp.isSlamModuleRunning():
+            break
+        import time
+        time.sleep(0.05)
+    assert youth_icp.isSlamModuleRunning() == 1
+    frames, _ = youth_synth.sequence(0, 2)
+    assert youth_icp.processSlamFrame(frames[0], None, 640, 480, 0) == 1
+    assert youth_icp.processSlamFrame(frames[1], None, 640, 480, 33) == 1
+    assert youth_icp.slam_wait_idle(20000) == 1
+    youth_icp.stopSlamModule()
+    t.join(timeout=10)
+    assert not t.is_alive()

@@ -1,0 +1,171 @@
+"""CPU tests of the oracle (the checker itself): pinned against the reference's
+known-answer back-projection table, cross-checked against numpy/scipy, and
+regression-pinned against the committed golden fixtures."""
+import os
+
+import numpy as np
+import pytest
+import scipy.linalg
+
+import oracle
+import youth_synth
+from conftest import GOLDEN
+
+PAIR_CASES = ["pair_80x60", "pair_160x120", "pair_97x53"]
+
+
+def _load(name):
+    return np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+
+
+def _K(arr):
+    return oracle.OracleIntrinsics(*[float(v) for v in arr])
+
+
+def f32bits(x):
+    return int(np.float32(x).view(np.uint32))
+
+
+def test_backproject_kat_pinned_to_reference():
+    """SURVEY.md §4 KAT (reference formula viewerModule.c:343-345, bit patterns)."""
+    table = _load("kat_backproject")["table"]
+    for W, H, u, v, d, xb, yb, zb in table.tolist():
+        depth = np.zeros((H, W), np.int16)
+        depth[v, u] = d
+        X, Y, Z = oracle.backproject(depth)
+        assert (f32bits(X[v, u]), f32bits(Y[v, u]), f32bits(Z[v, u])) == (xb, yb, zb), (u, v, d)
+
+
+def test_backproject_matches_viewer_expression():
+    """Restate viewerModule.c:343-345 in numpy fp32, all pixels, random depths."""
+    rng = np.random.default_rng(1)
+    H, W = 48, 64
+    depth = rng.integers(-200, 32768, size=(H, W)).astype(np.int16)
+    X, Y, Z = oracle.backproject(depth)
+    d = depth.astype(np.int32)
+    u = np.arange(W, dtype=np.int32)[None, :].repeat(H, 0)
+    v = np.arange(H, dtype=np.int32)[:, None].repeat(W, 1)
+    z = (d.astype(np.float32) / np.float32(1000.0)).astype(np.float32)
+    x = ((u - W // 2).astype(np.float32) * z) / np.float32(570.3)
+    y = ((v - H // 2).astype(np.float32) * z) / np.float32(570.3)
+    valid = d > 0
+    assert np.array_equal(Z.view(np.uint32), np.where(valid, z, 0).astype(np.float32).view(np.uint32))
+    assert np.array_equal(X[valid].view(np.uint32), x[valid].view(np.uint32))
+    assert np.array_equal(Y[valid].view(np.uint32), y[valid].view(np.uint32))
+    assert not X[~valid].any() and not Y[~valid].any()
+
+
+def test_se3_exp_matches_scipy_expm():
+    rng = np.random.default_rng(2)
+    for scale in (1e-9, 1e-4, 0.05, 1.0):
+        xi = rng.normal(size=6) * scale
+        E = oracle.se3_exp(xi)
+        w, t = xi[:3], xi[3:]
+        M = np.zeros((4, 4))
+        M[:3, :3] = [[0, -w[2], w[1]], [w[2], 0, -w[0]], [-w[1], w[0], 0]]
+        M[:3, 3] = t
+        assert np.abs(E - scipy.linalg.expm(M)).max() < 1e-12
+
+
+def test_solve_matches_numpy():
+    rng = np.random.default_rng(3)
+    for _ in range(5):
+        J = rng.normal(size=(500, 6))
+        r = rng.normal(size=500)
+        A = J.T @ J
+        b = J.T @ r
+        neq = np.zeros(29)
+        neq[:21] = A[np.triu_indices(6)]
+        neq[21:27] = b
+        neq[27] = r @ r
+        neq[28] = 500
+        xi, st = oracle.solve(neq)
+        assert st == 0
+        assert np.abs(xi - np.linalg.solve(A, -b)).max() < 1e-10
+
+
+def test_solve_degenerate_cases():
+    neq = np.zeros(29)
+    neq[28] = 3
+    xi, st = oracle.solve(neq)
+    assert st == 2 and not xi.any()          # fewer than 6 correspondences
+    neq[28] = 100
+    xi, st = oracle.solve(neq)                # all-zero A: singular
+    assert st == 1 and not xi.any()
+    J = np.zeros((100, 6))
+    J[:, 5] = 1.0                             # one plane: rank 1
+    A = J.T @ J
+    neq[:21] = A[np.triu_indices(6)]
+    assert oracle.solve(neq)[1] == 1
+
+
+def test_identity_pair_gives_exact_identity():
+    src, dst, _ = youth_synth.pairs(7, 1, 160, 120)
+    T64, T32, st, stats = oracle.align(dst[0], dst[0], iters=3)
+    assert st == 0
+    assert np.array_equal(T64, np.eye(4))
+    assert stats[0, 1] == 0.0
+
+
+def test_known_motion_recovered_noise_free():
+    src, dst, Tgt = youth_synth.pairs(0, 3, flags=0)
+    for p in range(3):
+        T64, _, st, _ = oracle.align(src[p], dst[p], iters=10)
+        D = np.linalg.inv(Tgt[p]) @ T64
+        ang = np.degrees(np.arccos(np.clip((np.trace(D[:3, :3]) - 1) / 2, -1, 1)))
+        assert st == 0
+        assert ang < 0.005 and np.linalg.norm(D[:3, 3]) < 1e-4
+
+
+def test_empty_frames_status():
+    z = np.zeros((60, 80), np.int16)
+    T64, _, st, stats = oracle.align(z, z, iters=2)
+    assert st == 2 and np.array_equal(T64, np.eye(4)) and not stats[:, 0].any()
+
+
+@pytest.mark.parametrize("name", PAIR_CASES)
+def test_oracle_reproduces_golden(name):
+    g = _load(name)
+    K = _K(g["K"])
+    src, dst = g["src"], g["dst"]
+    X, Y, Z = oracle.backproject(src, K)
+    assert np.array_equal(np.stack([X, Y, Z]).view(np.uint32), g["src_xyz"].view(np.uint32))
+    tX, tY, tZ = oracle.backproject(dst, K)
+    N = np.stack(oracle.normals(tX, tY, tZ))
+    assert np.array_equal(N.view(np.uint32), g["dst_nrm"].view(np.uint32))
+    I12 = np.eye(4, dtype=np.float32)[:3]
+    dist = float(g["dist_thresh"])
+    assert np.array_equal(oracle.associate(src, dst, I12, K, dist), g["idx_identity"])
+    assert np.array_equal(oracle.reduce(src, dst, I12, K, dist), g["neq_identity"])
+    T64, T32, st, stats = oracle.align(src, dst, K, int(g["iters"]), dist)
+    assert np.array_equal(T64, g["T64"]) and np.array_equal(T32, g["T32"])
+    assert st == int(g["status"])
+
+
+def test_golden_poses_near_ground_truth():
+    for name in PAIR_CASES:
+        g = _load(name)
+        D = np.linalg.inv(g["T_gt"]) @ g["T64"]
+        assert np.linalg.norm(D[:3, 3]) < 1e-2, name   # sanity (tiny noisy frames), not parity
+
+
+def test_oracle_normals_unit_and_oriented():
+    g = _load("pair_160x120")
+    N = g["dst_nrm"]
+    P = g["dst_xyz"]
+    valid = np.any(N != 0, axis=0)
+    assert valid.mean() > 0.8
+    norm = np.sqrt((N.astype(np.float64) ** 2).sum(0))[valid]
+    assert np.abs(norm - 1).max() < 1e-6
+    assert (np.einsum("kij,kij->ij", N, P)[valid] <= 0).all()
+    # border and invalid-neighbour pixels carry no normal
+    assert not N[:, 0, :].any() and not N[:, -1, :].any()
+    assert not N[:, :, 0].any() and not N[:, :, -1].any()
+
+
+def test_batch_openmp_matches_single():
+    src, dst, _ = youth_synth.pairs(3, 4, 160, 120)
+    Tb, st = oracle.align_batch(src, dst, iters=5, n_threads=4)
+    for p in range(4):
+        T64, _, s1, _ = oracle.align(src[p], dst[p], iters=5)
+        assert np.array_equal(Tb[p], T64) and st[p] == s1
