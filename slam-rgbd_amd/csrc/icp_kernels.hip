@@ -72,12 +72,16 @@ __device__ __forceinline__ void backproject(int d, int u, int v, const Intr& K,
 
 // ------------------------------------------------------------------ k_prep --
 // grid (ceil(W/64), ceil(H/16), n_frames); frame f reads depth from
-// depth_a + f*N when f < n_a, else depth_b + (f - n_a)*N, and writes
-// workspace frame out0 + f.  Frames with f >= nrm_first also get normals.
+// depth_a + f*N when f < n_a, else depth_b + (f - n_a)*N, and fills workspace
+// frame out0 + f:
+//   f <  xyz_end   -> SoA XYZ planes (the frame is a source);
+//   f >= rec_first -> 16-byte records {z, nx, ny, nz} (the frame is a target),
+//                     normals from the (16+2) x (64+2) back-projected
+//                     neighbourhood staged in LDS.
 __global__ __launch_bounds__(kPrepThreads) void k_prep(
-    const int16_t* __restrict__ depth_a, const int16_t* __restrict__ depth_b,
-    int n_a, int out0, int nrm_first, int W, int H, size_t P, Intr K,
-    float* __restrict__ xyz, float* __restrict__ nrm)
+    const int16_t* __restrict__ depth_a, const int16_t* __restrict__ depth_b, int n_a,
+    int out0, int rec_first, int xyz_end, int W, int H, size_t P, Intr K,
+    float* __restrict__ xyz, float4* __restrict__ recs)
 {
     __shared__ float sX[kLdsH][kLdsW];
     __shared__ float sY[kLdsH][kLdsW];
@@ -86,17 +90,18 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(
     const int f = blockIdx.z;
     const size_t N = (size_t)W * (size_t)H;
     const int16_t* dep = (f < n_a) ? depth_a + (size_t)f * N : depth_b + (size_t)(f - n_a) * N;
-    const size_t fo = (size_t)(out0 + f) * 3 * P;
-    float* X = xyz + fo;
+    float* X = xyz + (size_t)(out0 + f) * 3 * P;
     float* Y = X + P;
     float* Z = Y + P;
+    float4* R = recs + (size_t)(out0 + f) * P;
+    const bool want_xyz = f < xyz_end;
     const int x0 = blockIdx.x * kTileW;
     const int y0 = blockIdx.y * kTileH;
     const int tx = threadIdx.x & 63;
     const int ty = threadIdx.x >> 6;
 
-    if (f < nrm_first) {
-        // Source frame: XYZ only, no neighbourhood needed.
+    if (f < rec_first) {
+        // Source-only frame: XYZ planes, no neighbourhood needed.
 #pragma unroll
         for (int k = 0; k < kTileH / 4; ++k) {
             const int gx = x0 + tx, gy = y0 + ty + 4 * k;
@@ -126,9 +131,6 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(
     }
     __syncthreads();
 
-    float* NXp = nrm + fo;
-    float* NYp = NXp + P;
-    float* NZp = NYp + P;
 #pragma unroll
     for (int k = 0; k < kTileH / 4; ++k) {
         const int row = ty + 4 * k;
@@ -137,9 +139,11 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(
         const size_t i = (size_t)gy * W + gx;
         const int ly = row + 1, lx = tx + 1;
         const float px = sX[ly][lx], py = sY[ly][lx], pz = sZ[ly][lx];
-        X[i] = px;
-        Y[i] = py;
-        Z[i] = pz;
+        if (want_xyz) {
+            X[i] = px;
+            Y[i] = py;
+            Z[i] = pz;
+        }
         float nx = 0.0f, ny = 0.0f, nz = 0.0f;
         const bool inner = gx > 0 && gy > 0 && gx < W - 1 && gy < H - 1;
         if (inner) {
@@ -169,131 +173,109 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(
                 }
             }
         }
-        NXp[i] = nx;
-        NYp[i] = ny;
-        NZp[i] = nz;
+        R[i] = make_float4(pz, nx, ny, nz);
     }
 }
 
 // ---------------------------------------------------------------- k_reduce --
+// Fused transform -> project -> gate -> residual -> Jacobian -> fp64
+// normal-equation accumulation (spec a7-a9).  Data layout:
+//   source  SoA XYZ planes: three dwordx4 loads per lane per 4 pixels;
+//   target  one 16-byte record {z, nx, ny, nz} per pixel: ONE aligned dwordx4
+//           fetch per correspondence; the target's x, y are recomputed from z
+//           with k_prep's back-projection expression, so they are
+//           bit-identical to the planes k_prep would have stored.
+// 28 B/px per iteration instead of 36 B/px with six 4-byte gathers
+// (tools/kbench: 175 -> 117 us for 64 pairs; sums bit-identical).
+// Accumulators are fp64 fed with exact fp32 products: the result equals the
+// oracle's row-major fp64 sum up to fp64 summation order.
 struct PairMap {
     int src0, tgt0;  // pair p: source frame src0 + p, target frame tgt0 + p
 };
 
-template <bool kAssoc>
-__device__ __forceinline__ void accumulate_pixel(
-    float sx, float sy, float sz, const float* __restrict__ T, const Intr& K, int W,
-    int H, float thr2, const float* __restrict__ tX, const float* __restrict__ tY,
-    const float* __restrict__ tZ, const float* __restrict__ nX,
-    const float* __restrict__ nY, const float* __restrict__ nZ, double* acc,
-    int32_t* assoc_slot)
+template <typename Acc>
+__device__ __forceinline__ void acc_fma(Acc& a, float x, float y);
+template <>
+__device__ __forceinline__ void acc_fma<double>(double& a, float x, float y)
 {
-    // spec a7: P' = R P + t, fixed order, no FMA (-ffp-contract=off)
-    const float qx = ((T[0] * sx + T[1] * sy) + T[2] * sz) + T[3];
-    const float qy = ((T[4] * sx + T[5] * sy) + T[6] * sz) + T[7];
-    const float qz = ((T[8] * sx + T[9] * sy) + T[10] * sz) + T[11];
-    int j = -1;
-    if (sz > 0.0f && qz > 0.0f) {
-        const float fu = floorf((((K.fx * qx) / qz) + K.cx) + 0.5f);
-        const float fv = floorf((((K.fy * qy) / qz) + K.cy) + 0.5f);
-        if (fu >= 0.0f && fu < (float)W && fv >= 0.0f && fv < (float)H)
-            j = (int)fv * W + (int)fu;
-    }
-    float nx = 0.0f, ny = 0.0f, nz = 0.0f, dx = 0.0f, dy = 0.0f, dz = 0.0f;
-    if (j >= 0) {
-        const float tz = tZ[j];
-        nx = nX[j];
-        ny = nY[j];
-        nz = nZ[j];
-        dx = qx - tX[j];
-        dy = qy - tY[j];
-        dz = qz - tz;
-        const float d2 = (dx * dx + dy * dy) + dz * dz;
-        const bool nvalid = !(nx == 0.0f && ny == 0.0f && nz == 0.0f);
-        if (!(tz > 0.0f) || !nvalid || !(d2 < thr2)) j = -1;
-    }
-    if (kAssoc) *assoc_slot = j;
-    if (j < 0) return;
-    // spec a8: r = n.(P' - P_t); J = [P' x n, n]
-    const float r = (nx * dx + ny * dy) + nz * dz;
-    float Jf[6];
-    Jf[0] = qy * nz - qz * ny;
-    Jf[1] = qz * nx - qx * nz;
-    Jf[2] = qx * ny - qy * nx;
-    Jf[3] = nx;
-    Jf[4] = ny;
-    Jf[5] = nz;
-    double J[6];
-#pragma unroll
-    for (int a = 0; a < 6; ++a) J[a] = (double)Jf[a];
-    const double rd = (double)r;
-    // spec a9: products of fp32 values are exact in fp64; one rounding per add
-    int k = 0;
-#pragma unroll
-    for (int a = 0; a < 6; ++a)
-#pragma unroll
-        for (int b = a; b < 6; ++b) {
-            acc[k] = fma(J[a], J[b], acc[k]);
-            ++k;
-        }
-#pragma unroll
-    for (int a = 0; a < 6; ++a) acc[21 + a] = fma(J[a], rd, acc[21 + a]);
-    acc[27] = fma(rd, rd, acc[27]);
-    acc[28] += 1.0;
+    a = fma((double)x, (double)y, a);
 }
 
-// grid (nblk, n_pairs); workgroup b of pair p covers pixels
-// [b*chunk, min((b+1)*chunk, N)); chunk is a multiple of kRedStep.
 template <bool kAssoc>
-__global__ __launch_bounds__(kRedThreads) void k_reduce(
-    const float* __restrict__ xyz, const float* __restrict__ nrm, size_t P, PairMap pm,
-    const float* __restrict__ T32, int W, int H, Intr K, float thr2, int chunk,
-    double* __restrict__ partials, int32_t* __restrict__ assoc)
+__device__ __forceinline__ void process4(const float xs[4], const float ys[4],
+                                         const float zs[4], int i, int end,
+                                         const float* __restrict__ T, const Intr& K, int W, int H,
+                                         float thr2, const float4* __restrict__ rec, double* acc,
+                                         int32_t* __restrict__ arow)
 {
-    __shared__ double red[kRedThreads / 64][kNeq];
-    const int p = blockIdx.y;
-    const int b = blockIdx.x;
-    const int nblk = gridDim.x;
-    const int N = W * H;
-    const float* sX = xyz + (size_t)(pm.src0 + p) * 3 * P;
-    const float* sY = sX + P;
-    const float* sZ = sY + P;
-    const size_t to = (size_t)(pm.tgt0 + p) * 3 * P;
-    const float* tX = xyz + to;
-    const float* tY = tX + P;
-    const float* tZ = tY + P;
-    const float* nX = nrm + to;
-    const float* nY = nX + P;
-    const float* nZ = nY + P;
-    float T[12];
+    // spec a7: P' = R P + t, fixed order, no FMA; projective association
+    float qx[4], qy[4], qz[4], fu[4], fv[4];
+    int j[4];
 #pragma unroll
-    for (int i = 0; i < 12; ++i) T[i] = T32[p * 12 + i];
-
-    double acc[kNeq];
-#pragma unroll
-    for (int k = 0; k < kNeq; ++k) acc[k] = 0.0;
-
-    const int start = b * chunk;
-    const int end = min(start + chunk, N);
-    int32_t* arow = kAssoc ? assoc + (size_t)p * N : nullptr;
-    for (int i = start + threadIdx.x * 4; i < end; i += kRedStep) {
-        const float4 x4 = *reinterpret_cast<const float4*>(sX + i);
-        const float4 y4 = *reinterpret_cast<const float4*>(sY + i);
-        const float4 z4 = *reinterpret_cast<const float4*>(sZ + i);
-        const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
-        const float ys[4] = {y4.x, y4.y, y4.z, y4.w};
-        const float zs[4] = {z4.x, z4.y, z4.z, z4.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            int32_t dummy;
-            const bool in = (i + q) < end;
-            accumulate_pixel<kAssoc>(xs[q], ys[q], in ? zs[q] : 0.0f, T, K, W, H, thr2, tX,
-                                     tY, tZ, nX, nY, nZ, acc,
-                                     (kAssoc && in) ? arow + i + q : &dummy);
+    for (int q = 0; q < 4; ++q) {
+        const float sx = xs[q], sy = ys[q], sz = (i + q) < end ? zs[q] : 0.0f;
+        qx[q] = ((T[0] * sx + T[1] * sy) + T[2] * sz) + T[3];
+        qy[q] = ((T[4] * sx + T[5] * sy) + T[6] * sz) + T[7];
+        qz[q] = ((T[8] * sx + T[9] * sy) + T[10] * sz) + T[11];
+        j[q] = -1;
+        fu[q] = 0.0f;
+        fv[q] = 0.0f;
+        if (sz > 0.0f && qz[q] > 0.0f) {
+            const float u = floorf((((K.fx * qx[q]) / qz[q]) + K.cx) + 0.5f);
+            const float v = floorf((((K.fy * qy[q]) / qz[q]) + K.cy) + 0.5f);
+            if (u >= 0.0f && u < (float)W && v >= 0.0f && v < (float)H) {
+                j[q] = (int)v * W + (int)u;
+                fu[q] = u;
+                fv[q] = v;
+            }
         }
     }
+    // all four fetches issued back to back from clamped indices (no branch)
+    float4 t[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) t[q] = rec[j[q] >= 0 ? j[q] : 0];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float tz = t[q].x;
+        const float tx = ((fu[q] - K.cx) * tz) / K.fx;  // = k_prep's X of pixel (u', v')
+        const float ty = ((fv[q] - K.cy) * tz) / K.fy;
+        const float nx = t[q].y, ny = t[q].z, nz = t[q].w;
+        const float dx = qx[q] - tx, dy = qy[q] - ty, dz = qz[q] - tz;
+        const float d2 = (dx * dx + dy * dy) + dz * dz;
+        const bool nvalid = !(nx == 0.0f && ny == 0.0f && nz == 0.0f);
+        const bool ok = j[q] >= 0 && tz > 0.0f && nvalid && d2 < thr2;
+        if (kAssoc && (i + q) < end) arow[i + q] = ok ? j[q] : -1;
+        // spec a8: r = n.(P' - P_t); J = [P' x n, n]  (zeros when unmatched)
+        const float n0 = ok ? nx : 0.0f, n1 = ok ? ny : 0.0f, n2 = ok ? nz : 0.0f;
+        const float r = ok ? (nx * dx + ny * dy) + nz * dz : 0.0f;
+        float Jf[6];
+        Jf[0] = qy[q] * n2 - qz[q] * n1;
+        Jf[1] = qz[q] * n0 - qx[q] * n2;
+        Jf[2] = qx[q] * n1 - qy[q] * n0;
+        Jf[3] = n0;
+        Jf[4] = n1;
+        Jf[5] = n2;
+        // spec a9: fp32 products are exact in fp64; one rounding per add
+        int k = 0;
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+            for (int b = a; b < 6; ++b) {
+                acc_fma<double>(acc[k], Jf[a], Jf[b]);
+                ++k;
+            }
+#pragma unroll
+        for (int a = 0; a < 6; ++a) acc_fma<double>(acc[21 + a], Jf[a], r);
+        acc_fma<double>(acc[27], r, r);
+        acc[28] += ok ? 1.0 : 0.0;
+    }
+}
 
-    // wave butterfly (lane-symmetric, so every lane holds the same sum)
+// Wave butterfly (lane-symmetric: every lane ends with the same sum), then
+// waves in fixed order through LDS; one 29-double partial per workgroup.
+__device__ __forceinline__ void block_reduce_store(double* acc, double (*red)[kNeq],
+                                                   double* __restrict__ out)
+{
 #pragma unroll
     for (int k = 0; k < kNeq; ++k) {
         double v = acc[k];
@@ -312,9 +294,50 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce(
         double s = red[0][k];
 #pragma unroll
         for (int w = 1; w < kRedThreads / 64; ++w) s += red[w][k];
-        partials[((size_t)p * nblk + b) * kNeq + k] = s;
+        out[k] = s;
     }
 }
+
+// grid (nblk, n_pairs); workgroup b of pair p covers pixels
+// [b*chunk, min((b+1)*chunk, N)); chunk is a multiple of kRedStep.
+template <bool kAssoc>
+__global__ __launch_bounds__(kRedThreads) void k_reduce(
+    const float* __restrict__ xyz, const float4* __restrict__ recs, size_t P, PairMap pm,
+    const float* __restrict__ T32, int W, int H, Intr K, float thr2, int chunk,
+    double* __restrict__ partials, int32_t* __restrict__ assoc)
+{
+    __shared__ double red[kRedThreads / 64][kNeq];
+    const int p = blockIdx.y;
+    const int b = blockIdx.x;
+    const int N = W * H;
+    const float* sX = xyz + (size_t)(pm.src0 + p) * 3 * P;
+    const float* sY = sX + P;
+    const float* sZ = sY + P;
+    const float4* rec = recs + (size_t)(pm.tgt0 + p) * P;
+    float T[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) T[k] = T32[p * 12 + k];
+
+    double acc[kNeq];
+#pragma unroll
+    for (int k = 0; k < kNeq; ++k) acc[k] = 0.0;
+
+    const int start = b * chunk;
+    const int end = min(start + chunk, N);
+    int32_t* arow = kAssoc ? assoc + (size_t)p * N : nullptr;
+    for (int i = start + threadIdx.x * 4; i < end; i += kRedStep) {
+        // i % 4 == 0 and P >= N + 4: the float4 never leaves the zeroed pad
+        const float4 x4 = *reinterpret_cast<const float4*>(sX + i);
+        const float4 y4 = *reinterpret_cast<const float4*>(sY + i);
+        const float4 z4 = *reinterpret_cast<const float4*>(sZ + i);
+        const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
+        const float ys[4] = {y4.x, y4.y, y4.z, y4.w};
+        const float zs[4] = {z4.x, z4.y, z4.z, z4.w};
+        process4<kAssoc>(xs, ys, zs, i, end, T, K, W, H, thr2, rec, acc, arow);
+    }
+    block_reduce_store(acc, red, partials + ((size_t)p * gridDim.x + b) * kNeq);
+}
+
 
 // ----------------------------------------------------------------- k_solve --
 // LDL^T + SE(3) exp, same algorithm and evaluation order as oracle_solve /
@@ -543,7 +566,7 @@ struct youth_icp_ctx {
 
     int16_t* d_depth = nullptr;  // [max_frames][N] staging for host-side APIs
     float* d_xyz = nullptr;      // [max_frames][3][P]
-    float* d_nrm = nullptr;      // [max_frames][3][P]
+    float4* d_rec = nullptr;     // [max_frames][P] target records {z, nx, ny, nz}
     double* d_T64 = nullptr;     // [max_frames][16]
     float* d_T32 = nullptr;      // [max_frames][12]
     int32_t* d_status = nullptr; // [max_frames]
@@ -652,15 +675,15 @@ static int ev_harvest(youth_icp_ctx* c)
 
 // Launch k_prep for frames [out0, out0 + n_frames).
 static int launch_prep(youth_icp_ctx* c, hipStream_t s, const int16_t* da, const int16_t* db,
-                       int n_a, int out0, int n_frames, int nrm_first)
+                       int n_a, int out0, int n_frames, int rec_first, int xyz_end)
 {
     if (n_frames <= 0) return YOUTH_OK;
     dim3 grid((c->W + kTileW - 1) / kTileW, (c->H + kTileH - 1) / kTileH, n_frames);
     EventPair ep{};
     int rc = ev_begin(c, s, &ep, 2);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_prep, grid, dim3(kPrepThreads), 0, s, da, db, n_a, out0, nrm_first,
-                       c->W, c->H, c->P, c->K, c->d_xyz, c->d_nrm);
+    hipLaunchKernelGGL(k_prep, grid, dim3(kPrepThreads), 0, s, da, db, n_a, out0, rec_first,
+                       xyz_end, c->W, c->H, c->P, c->K, c->d_xyz, c->d_rec);
     HIP_TRY(hipGetLastError());
     return ev_end(c, s, &ep);
 }
@@ -680,11 +703,11 @@ static int launch_reduce(youth_icp_ctx* c, hipStream_t s, PairMap pm, int n_pair
     if (assoc) {
         rc = ensure_assoc(c);
         if (rc) return rc;
-        hipLaunchKernelGGL(k_reduce<true>, grid, dim3(kRedThreads), 0, s, c->d_xyz, c->d_nrm,
+        hipLaunchKernelGGL(k_reduce<true>, grid, dim3(kRedThreads), 0, s, c->d_xyz, c->d_rec,
                            c->P, pm, c->d_T32, c->W, c->H, c->K, thr2, chunk, c->d_partials,
                            c->d_assoc);
     } else {
-        hipLaunchKernelGGL(k_reduce<false>, grid, dim3(kRedThreads), 0, s, c->d_xyz, c->d_nrm,
+        hipLaunchKernelGGL(k_reduce<false>, grid, dim3(kRedThreads), 0, s, c->d_xyz, c->d_rec,
                            c->P, pm, c->d_T32, c->W, c->H, c->K, thr2, chunk, c->d_partials,
                            (int32_t*)nullptr);
     }
@@ -788,7 +811,7 @@ void youth_icp_destroy(youth_icp_ctx* c)
             (void)hipEventDestroy(e.a);
             (void)hipEventDestroy(e.b);
         }
-    void* bufs[] = {c->d_depth, c->d_xyz,   c->d_nrm,      c->d_T64, c->d_T32,   c->d_status,
+    void* bufs[] = {c->d_depth, c->d_xyz,   c->d_rec,      c->d_T64, c->d_T32,   c->d_status,
                     c->d_Tinit, c->d_stats, c->d_partials, c->d_neq, c->d_assoc, c->d_Tout};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -829,13 +852,14 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         return fail("hipStreamCreate", e);
     const size_t MF = (size_t)max_frames;
     const size_t plane_bytes = 3 * c->P * sizeof(float) * MF;
+    const size_t rec_bytes = c->P * sizeof(float4) * MF;
     if ((e = hipMalloc(&c->d_depth, MF * c->N * sizeof(int16_t))) != hipSuccess)
         return fail("hipMalloc depth", e);
     if ((e = hipMalloc(&c->d_xyz, plane_bytes)) != hipSuccess) return fail("hipMalloc xyz", e);
-    if ((e = hipMalloc(&c->d_nrm, plane_bytes)) != hipSuccess) return fail("hipMalloc nrm", e);
+    if ((e = hipMalloc(&c->d_rec, rec_bytes)) != hipSuccess) return fail("hipMalloc rec", e);
     // the pad beyond N of every plane must read as an invalid point (Z = 0)
     if ((e = hipMemset(c->d_xyz, 0, plane_bytes)) != hipSuccess) return fail("memset xyz", e);
-    if ((e = hipMemset(c->d_nrm, 0, plane_bytes)) != hipSuccess) return fail("memset nrm", e);
+    if ((e = hipMemset(c->d_rec, 0, rec_bytes)) != hipSuccess) return fail("memset rec", e);
     if ((e = hipMalloc(&c->d_T64, MF * 16 * sizeof(double))) != hipSuccess)
         return fail("hipMalloc T64", e);
     if ((e = hipMalloc(&c->d_T32, MF * 12 * sizeof(float))) != hipSuccess)
@@ -866,7 +890,7 @@ int youth_icp_align_pairs_device(youth_icp_ctx* c, const int16_t* d_src, const i
     if (rc) return rc;
     hipStream_t s = pick_stream(c, stream);
     // frames [0, n): sources (XYZ only); [n, 2n): targets (XYZ + normals)
-    rc = launch_prep(c, s, d_src, d_dst, n_pairs, 0, 2 * n_pairs, n_pairs);
+    rc = launch_prep(c, s, d_src, d_dst, n_pairs, 0, 2 * n_pairs, n_pairs, n_pairs);
     if (rc) return rc;
     rc = run_iterations(c, s, PairMap{0, n_pairs}, n_pairs, T_init);
     if (rc) return rc;
@@ -881,7 +905,7 @@ int youth_icp_align_sequence_device(youth_icp_ctx* c, const int16_t* d_frames, i
     int rc = bind_device(c);
     if (rc) return rc;
     hipStream_t s = pick_stream(c, stream);
-    rc = launch_prep(c, s, d_frames, d_frames, n_frames, 0, n_frames, 0);
+    rc = launch_prep(c, s, d_frames, d_frames, n_frames, 0, n_frames, 0, n_frames);
     if (rc) return rc;
     // pair k: source frame k+1, target frame k
     rc = run_iterations(c, s, PairMap{1, 0}, n_frames - 1, nullptr);
@@ -979,16 +1003,21 @@ int youth_icp_prepare_host(youth_icp_ctx* c, const int16_t* depth, int n_frames,
     HIP_TRY(hipMemcpyAsync(c->d_depth, depth, (size_t)n_frames * N * sizeof(int16_t),
                            hipMemcpyHostToDevice, s));
     rc = launch_prep(c, s, c->d_depth, c->d_depth, n_frames, 0, n_frames,
-                     want_normals ? 0 : n_frames);
+                     want_normals ? 0 : n_frames, n_frames);
     if (rc) return rc;
     float* outs[6] = {X, Y, Z, NX, NY, NZ};
     for (int f = 0; f < n_frames; ++f)
         for (int k = 0; k < 6; ++k) {
             if (!outs[k] || (k >= 3 && !want_normals)) continue;
-            const float* base = (k < 3 ? c->d_xyz : c->d_nrm) + (size_t)f * 3 * c->P +
-                                (size_t)(k % 3) * c->P;
-            HIP_TRY(hipMemcpyAsync(outs[k] + (size_t)f * N, base, N * sizeof(float),
-                                   hipMemcpyDeviceToHost, s));
+            float* dst = outs[k] + (size_t)f * N;
+            if (k < 3) {
+                const float* base = c->d_xyz + (size_t)f * 3 * c->P + (size_t)k * c->P;
+                HIP_TRY(hipMemcpyAsync(dst, base, N * sizeof(float), hipMemcpyDeviceToHost, s));
+            } else {  // component k-2 of the {z, nx, ny, nz} records
+                const float* base = reinterpret_cast<const float*>(c->d_rec + (size_t)f * c->P) + (k - 2);
+                HIP_TRY(hipMemcpy2DAsync(dst, sizeof(float), base, sizeof(float4), sizeof(float), N,
+                                         hipMemcpyDeviceToHost, s));
+            }
         }
     HIP_TRY(hipStreamSynchronize(s));
     return YOUTH_OK;
@@ -1005,7 +1034,7 @@ int youth_icp_reduce_host(youth_icp_ctx* c, const int16_t* src, const int16_t* d
     const size_t N = c->N;
     HIP_TRY(hipMemcpyAsync(c->d_depth, src, N * sizeof(int16_t), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(c->d_depth + N, dst, N * sizeof(int16_t), hipMemcpyHostToDevice, s));
-    rc = launch_prep(c, s, c->d_depth, c->d_depth, 2, 0, 2, 1);
+    rc = launch_prep(c, s, c->d_depth, c->d_depth, 2, 0, 2, 1, 1);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(c->d_T32, T12, 12 * sizeof(float), hipMemcpyHostToDevice, s));
     int nb = 0;
@@ -1102,7 +1131,7 @@ int youth_icp_track_frame(youth_icp_ctx* c, const int16_t* depth, const double* 
     const int slot = c->track_ref == 0 ? 1 : 0;
     HIP_TRY(hipMemcpyAsync(c->d_depth + (size_t)slot * N, depth, N * sizeof(int16_t),
                            hipMemcpyHostToDevice, s));
-    rc = launch_prep(c, s, c->d_depth + (size_t)slot * N, nullptr, 1, slot, 1, 0);
+    rc = launch_prep(c, s, c->d_depth + (size_t)slot * N, nullptr, 1, slot, 1, 0, 1);
     if (rc) return rc;
     int32_t st = 0;
     const int ref = c->track_ref;
