@@ -34,7 +34,7 @@ import youth_synth  # noqa: E402
 METRIC = "ICP frame-pair aligns/sec @640×480 (1/2/4/8 GPU); SE(3) err vs CPU ref"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
 BYTES_PER_PX_ITER = 36       # src XYZ 12 + tgt XYZ 12 + tgt normal 12
-KERNEL_BYTES_PER_PX = 28     # k_reduce's own minimum: src XYZ 12 + tgt record {z,n} 16
+KERNEL_BYTES_PER_PX = 18     # k_reduce own bytes: src depth 2 + tgt record {z,n} 16
 
 
 def parse():

@@ -124,6 +124,12 @@ const char* youth_icp_last_error(void);
 /* Number of visible HIP devices (0 when none; never fails). */
 int youth_icp_device_count(void);
 
+/* 1 when this context's back-projection divides use the 3-instruction
+ * sequence (proven equal to IEEE division on the whole pixel x depth domain
+ * by an on-device exhaustive check at creation), 0 for the IEEE path.
+ * Environment YOUTH_ICP_NO_FASTDIV=1 forces the IEEE path. */
+int youth_icp_fastdiv_enabled(youth_icp_ctx* ctx);
+
 /* One-shot host API:  aligns n_pairs independent pairs; src and
  * dst are [n_pairs][H][W] int16 host arrays.  T_out: [n_pairs][16] row-major
  * fp32 4x4 with P_dst = T * P_src.  assoc_out: nullable [n_pairs][H*W] int32
@@ -133,15 +139,18 @@ int youth_icp_align_batch(const int16_t* src, const int16_t* dst, int n_pairs,
                           int W, int H, const youth_intrinsics* K, int iters,
                           float* T_out, int32_t* assoc_out);
 
-/* Context: device workspace sized for max_frames frames of W x H.  The pair
- * batch API uses 2 frames per pair; the sequence API one per frame. */
+/* Context: device workspace sized for max_frames frames of W x H (target
+ * records + depth staging).  The pair API needs n_pairs <= max_frames, the
+ * sequence API n_frames - 1 <= max_frames, the one-shot host API stages
+ * 2 * n_pairs depth frames. */
 youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
                                 const youth_intrinsics* K,
                                 const youth_icp_params* P);
 void youth_icp_destroy(youth_icp_ctx* ctx);
 
 /* Device-resident align of n_pairs pairs.  d_src / d_dst: device pointers to
- * [n_pairs][H][W] int16.  T_init: nullable HOST [n_pairs][16] fp64 (identity
+ * [n_pairs][H][W] int16 (d_src is read by every iteration: keep it alive and
+ * unmodified until the align has completed on `stream`).  T_init: nullable HOST [n_pairs][16] fp64 (identity
  * if NULL).  d_T_out: nullable DEVICE [n_pairs][16] fp32.  stream: a
  * hipStream_t as void* (NULL = the context's own stream).  Asynchronous:
  * returns after enqueueing; use youth_icp_sync / youth_icp_get_poses. */

@@ -1,24 +1,30 @@
 // icp_kernels.hip — MI355X (gfx950) kernels of the RGBD frame-to-frame ICP path.
 //
-// Hot path, reference boundary
+// Hot path.  Reference boundary:
 // Youth.Source/AlgorithmModule/SLAM.cpp:54 (TrackRGBD, the pose maths this
-// replaces) and viewerModule.c:341-345 (the back-projection formula):
+// replaces) and viewerModule.c:341-345 (the back-projection formula).
 //
-//   k_prep    depth int16 -> XYZ planes (+ normals for target frames), one
-//             64x16 tile per workgroup, the (16+2)x(64+2) back-projected
-//             neighbourhood staged in LDS for the central-difference normals.
-//   k_reduce  fused transform -> project -> gate -> residual -> Jacobian ->
-//             29 fp64 accumulators per lane (exact fp32 products), wave
+//   k_prep    target frames: int16 depth -> one 16-byte record {z, nx, ny, nz}
+//             per pixel.  64x16 tiles; the (16+2) x (64+2) back-projected
+//             neighbourhood is staged in LDS for the central-difference
+//             normals.
+//   k_reduce  per ICP iteration: source pixels straight from the int16 depth
+//             (back-projected in registers), transform -> project -> ONE
+//             16-byte record fetch -> gate -> residual -> Jacobian -> 29 fp64
+//             accumulators per lane fed with exact fp32 products; wave
 //             butterfly + LDS across waves -> one 29-double partial per
-//             workgroup.  No atomics: deterministic.
-//   k_solve   one wave per pair: sums the workgroup partials in fixed order,
-//             LDL^T 6x6 solve, SE(3) exp, T <- exp(xi) T in fp64 on device,
-//             writes the fp32 pose for the next k_reduce.  No host round trip
-//             between iterations.
+//             workgroup.  No atomics: deterministic.  18 B/px/iteration.
+//   k_solve   one wave per pair: sums the partials in fixed order, LDL^T 6x6
+//             solve, SE(3) exp, T <- exp(xi) T in fp64 on device, fp32 pose
+//             for the next k_reduce.  No host round trip between iterations.
 //
 // Compiled with -ffp-contract=off: every fp32 expression rounds exactly as
 // written, identical to the C oracle (oracle/icp_oracle.c) — XYZ, normals and
-// association indices are bit-exact given the same fp32 pose.
+// association indices are bit-exact given the same fp32 pose.  The
+// back-projection divides use a 3-instruction sequence only after
+// k_verify_fastdiv has proven it equal to IEEE division on the ENTIRE domain
+// those divides can see (d in [1, 32767], u in [0, W), v in [0, H)); otherwise
+// the IEEE path is compiled in.
 
 #include <hip/hip_runtime.h>
 
@@ -37,9 +43,12 @@
 namespace {
 
 // ----------------------------------------------------------------- layout --
-// Frame f of the workspace: X plane at xyz + f*3*P, Y at +P, Z at +2P (SoA,
-// fp32); normals likewise in nrm.  P = plane stride = round_up(N + 4, 256)
-// floats, so float4 loads of the last pixels stay inside the (zeroed) pad.
+// Workspace frame f:
+//   recs + f*P            float4 {z, nx, ny, nz} per pixel (targets);
+//   xyz  + f*3*P (+P, +2P) optional X, Y, Z planes (stage-level API only).
+// P = plane stride = round_up(N + 4, 256); the pad is zeroed once, so a
+// clamped fetch or a float4 load past N reads an invalid point (z = 0).
+// Sources are read straight from the caller's int16 depth.
 constexpr int kTileW = 64;
 constexpr int kTileH = 16;
 constexpr int kPrepThreads = 256;
@@ -54,34 +63,72 @@ struct Intr {
     float fx, fy, cx, cy, ds;
 };
 
-__device__ __forceinline__ void backproject(int d, int u, int v, const Intr& K,
-                                            float& x, float& y, float& z)
+// RN(1/fx), RN(1/fy), RN(1/ds) for the verified 3-op division.
+struct FastK {
+    float rfx, rfy, rds;
+};
+
+// q = RN(n * rd); r = n - q d (exact, fma); q + r rd (one rounding).
+// Equal to RN(n / d) wherever k_verify_fastdiv found no mismatch.
+__device__ __forceinline__ float div_fast(float n, float d, float rd)
 {
-    // viewerModule.c:341-345 with explicit intrinsics (bit-identical for
-    // cx = W/2, cy = H/2, f = 570.3f, ds = 1000.0f).
-    if (d > 0) {
-        z = (float)d / K.ds;
-        x = (((float)u - K.cx) * z) / K.fx;
-        y = (((float)v - K.cy) * z) / K.fy;
-    } else {
-        x = 0.0f;
-        y = 0.0f;
-        z = 0.0f;
+    const float q = n * rd;
+    const float r = fmaf(-q, d, n);
+    return fmaf(r, rd, q);
+}
+
+template <bool kFast>
+__device__ __forceinline__ float bp_div(float n, float d, float rd)
+{
+    return kFast ? div_fast(n, d, rd) : n / d;
+}
+
+// viewerModule.c:341-345 with explicit intrinsics (bit-identical to the
+// viewer for cx = W/2, cy = H/2, f = 570.3f, ds = 1000.0f):
+//   valid iff d > 0;  z = d / ds;  x = ((u - cx) z) / fx;  y = ((v - cy) z) / fy
+template <bool kFast>
+__device__ __forceinline__ void backproject(int d, int u, int v, const Intr& K,
+                                            const FastK& F, float& x, float& y, float& z)
+{
+    const float zz = d > 0 ? bp_div<kFast>((float)d, K.ds, F.rds) : 0.0f;
+    x = bp_div<kFast>(((float)u - K.cx) * zz, K.fx, F.rfx);
+    y = bp_div<kFast>(((float)v - K.cy) * zz, K.fy, F.rfy);
+    z = zz;
+}
+
+// Exhaustive check of div_fast against IEEE division over the whole
+// back-projection domain: z = d/ds (d in [1, 32767]); ((u - cx) z)/fx
+// (u in [0, W)); ((v - cy) z)/fy (v in [0, H)).  Also covers the target
+// recompute in k_reduce (tz is some d/ds, u' in [0, W), v' in [0, H)).
+__global__ void k_verify_fastdiv(Intr K, FastK F, int W, int H, unsigned* bad)
+{
+    const int d = blockIdx.x * blockDim.x + threadIdx.x + 1;
+    if (d > 32767) return;
+    const float zi = (float)d / K.ds;
+    unsigned nb = (div_fast((float)d, K.ds, F.rds) != zi);
+    for (int u = blockIdx.y; u < W; u += gridDim.y) {
+        const float n = ((float)u - K.cx) * zi;
+        nb += (div_fast(n, K.fx, F.rfx) != n / K.fx);
     }
+    for (int v = blockIdx.y; v < H; v += gridDim.y) {
+        const float n = ((float)v - K.cy) * zi;
+        nb += (div_fast(n, K.fy, F.rfy) != n / K.fy);
+    }
+    if (nb) atomicAdd(bad, nb);
 }
 
 // ------------------------------------------------------------------ k_prep --
-// grid (ceil(W/64), ceil(H/16), n_frames); frame f reads depth from
-// depth_a + f*N when f < n_a, else depth_b + (f - n_a)*N, and fills workspace
-// frame out0 + f:
-//   f <  xyz_end   -> SoA XYZ planes (the frame is a source);
-//   f >= rec_first -> 16-byte records {z, nx, ny, nz} (the frame is a target),
-//                     normals from the (16+2) x (64+2) back-projected
-//                     neighbourhood staged in LDS.
-__global__ __launch_bounds__(kPrepThreads) void k_prep(
-    const int16_t* __restrict__ depth_a, const int16_t* __restrict__ depth_b, int n_a,
-    int out0, int rec_first, int xyz_end, int W, int H, size_t P, Intr K,
-    float* __restrict__ xyz, float4* __restrict__ recs)
+// grid (ceil(W/64), ceil(H/16), n_frames): frame f reads depth + f*N and
+// writes the target records of workspace frame out0 + f (and, when xyz is
+// non-null, its X/Y/Z planes: stage-level API only).  Normals (spec a6):
+// n = normalize((P(u+1)-P(u-1)) x (P(v+1)-P(v-1))); (0,0,0) on the 1-px
+// border, if the centre or any of the 4 neighbours is invalid, or if the
+// cross product is zero; oriented so n.P <= 0.
+template <bool kFast>
+__global__ __launch_bounds__(kPrepThreads) void k_prep(const int16_t* __restrict__ depth, int out0,
+                                                      int W, int H, size_t P, Intr K, FastK F,
+                                                      float4* __restrict__ recs,
+                                                      float* __restrict__ xyz)
 {
     __shared__ float sX[kLdsH][kLdsW];
     __shared__ float sY[kLdsH][kLdsW];
@@ -89,42 +136,20 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(
 
     const int f = blockIdx.z;
     const size_t N = (size_t)W * (size_t)H;
-    const int16_t* dep = (f < n_a) ? depth_a + (size_t)f * N : depth_b + (size_t)(f - n_a) * N;
-    float* X = xyz + (size_t)(out0 + f) * 3 * P;
-    float* Y = X + P;
-    float* Z = Y + P;
+    const int16_t* dep = depth + (size_t)f * N;
     float4* R = recs + (size_t)(out0 + f) * P;
-    const bool want_xyz = f < xyz_end;
     const int x0 = blockIdx.x * kTileW;
     const int y0 = blockIdx.y * kTileH;
     const int tx = threadIdx.x & 63;
     const int ty = threadIdx.x >> 6;
 
-    if (f < rec_first) {
-        // Source-only frame: XYZ planes, no neighbourhood needed.
-#pragma unroll
-        for (int k = 0; k < kTileH / 4; ++k) {
-            const int gx = x0 + tx, gy = y0 + ty + 4 * k;
-            if (gx < W && gy < H) {
-                const size_t i = (size_t)gy * W + gx;
-                float x, y, z;
-                backproject(dep[i], gx, gy, K, x, y, z);
-                X[i] = x;
-                Y[i] = y;
-                Z[i] = z;
-            }
-        }
-        return;
-    }
-
-    // Target frame: stage the back-projected (kTileH+2) x (kTileW+2) halo tile.
     for (int e = threadIdx.x; e < kLdsH * kLdsW; e += kPrepThreads) {
         const int ly = e / kLdsW;
         const int lx = e - ly * kLdsW;
         const int gx = x0 - 1 + lx, gy = y0 - 1 + ly;
         float x = 0.0f, y = 0.0f, z = 0.0f;
         if (gx >= 0 && gx < W && gy >= 0 && gy < H)
-            backproject(dep[(size_t)gy * W + gx], gx, gy, K, x, y, z);
+            backproject<kFast>(dep[(size_t)gy * W + gx], gx, gy, K, F, x, y, z);
         sX[ly][lx] = x;
         sY[ly][lx] = y;
         sZ[ly][lx] = z;
@@ -139,10 +164,11 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(
         const size_t i = (size_t)gy * W + gx;
         const int ly = row + 1, lx = tx + 1;
         const float px = sX[ly][lx], py = sY[ly][lx], pz = sZ[ly][lx];
-        if (want_xyz) {
+        if (xyz) {
+            float* X = xyz + (size_t)(out0 + f) * 3 * P;
             X[i] = px;
-            Y[i] = py;
-            Z[i] = pz;
+            X[P + i] = py;
+            X[2 * P + i] = pz;
         }
         float nx = 0.0f, ny = 0.0f, nz = 0.0f;
         const bool inner = gx > 0 && gy > 0 && gx < W - 1 && gy < H - 1;
@@ -178,104 +204,132 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(
 }
 
 // ---------------------------------------------------------------- k_reduce --
-// Fused transform -> project -> gate -> residual -> Jacobian -> fp64
-// normal-equation accumulation (spec a7-a9).  Data layout:
-//   source  SoA XYZ planes: three dwordx4 loads per lane per 4 pixels;
-//   target  one 16-byte record {z, nx, ny, nz} per pixel: ONE aligned dwordx4
-//           fetch per correspondence; the target's x, y are recomputed from z
-//           with k_prep's back-projection expression, so they are
-//           bit-identical to the planes k_prep would have stored.
-// 28 B/px per iteration instead of 36 B/px with six 4-byte gathers
-// (tools/kbench: 175 -> 117 us for 64 pairs; sums bit-identical).
-// Accumulators are fp64 fed with exact fp32 products: the result equals the
-// oracle's row-major fp64 sum up to fp64 summation order.
+// Spec a7-a9 for four consecutive source pixels per lane per step.
+//   source  int16 depth (2 B/px), back-projected in registers (8-byte load
+//           per lane when the frame is 8-byte aligned and N % 4 == 0);
+//   target  ONE aligned 16-byte record fetch {z, nx, ny, nz} per pixel; the
+//           target's x, y are recomputed from z with k_prep's expression, so
+//           they are bit-identical to what k_prep would have stored.
+// Branch-free: invalid lanes compute on safe values and are masked, so the
+// four fetches issue back to back.  Accumulators are fp64 fed with exact
+// fp32 products: the result equals the oracle's row-major fp64 sum up to
+// fp64 summation order.  (tools/kbench: 205 us for the first SoA version ->
+// 107 us for this one at 64 pairs, partial sums unchanged.)
 struct PairMap {
-    int src0, tgt0;  // pair p: source frame src0 + p, target frame tgt0 + p
+    int src0, tgt0;  // pair p: source depth frame src0 + p, target record frame tgt0 + p
 };
 
-template <typename Acc>
-__device__ __forceinline__ void acc_fma(Acc& a, float x, float y);
-template <>
-__device__ __forceinline__ void acc_fma<double>(double& a, float x, float y)
+template <bool kAligned>
+__device__ __forceinline__ short4 load_depth4(const int16_t* __restrict__ sD, int i, int end)
 {
-    a = fma((double)x, (double)y, a);
+    // i < end always here; kAligned => i % 4 == 0 and i + 3 < end
+    short4 d;
+    if (kAligned) {
+        d = *reinterpret_cast<const short4*>(sD + i);
+    } else {
+        d.x = sD[i];
+        d.y = (i + 1) < end ? sD[i + 1] : (short)0;
+        d.z = (i + 2) < end ? sD[i + 2] : (short)0;
+        d.w = (i + 3) < end ? sD[i + 3] : (short)0;
+    }
+    return d;
 }
 
-template <bool kAssoc>
-__device__ __forceinline__ void process4(const float xs[4], const float ys[4],
-                                         const float zs[4], int i, int end,
-                                         const float* __restrict__ T, const Intr& K, int W, int H,
-                                         float thr2, const float4* __restrict__ rec, double* acc,
-                                         int32_t* __restrict__ arow)
+template <bool kAssoc, bool kFast, bool kAligned>
+__global__ __launch_bounds__(kRedThreads) void k_reduce(
+    const int16_t* __restrict__ dsrc, const float4* __restrict__ recs, size_t P, PairMap pm,
+    const float* __restrict__ T32, int W, int H, Intr K, FastK F, float thr2, int chunk,
+    double* __restrict__ partials, int32_t* __restrict__ assoc)
 {
-    // spec a7: P' = R P + t, fixed order, no FMA; projective association
-    float qx[4], qy[4], qz[4], fu[4], fv[4];
-    int j[4];
+    __shared__ double red[kRedThreads / 64][kNeq];
+    const int p = blockIdx.y;
+    const int b = blockIdx.x;
+    const int N = W * H;
+    const int16_t* sD = dsrc + (size_t)(pm.src0 + p) * N;
+    const float4* rec = recs + (size_t)(pm.tgt0 + p) * P;
+    float T[12];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const float sx = xs[q], sy = ys[q], sz = (i + q) < end ? zs[q] : 0.0f;
-        qx[q] = ((T[0] * sx + T[1] * sy) + T[2] * sz) + T[3];
-        qy[q] = ((T[4] * sx + T[5] * sy) + T[6] * sz) + T[7];
-        qz[q] = ((T[8] * sx + T[9] * sy) + T[10] * sz) + T[11];
-        j[q] = -1;
-        fu[q] = 0.0f;
-        fv[q] = 0.0f;
-        if (sz > 0.0f && qz[q] > 0.0f) {
-            const float u = floorf((((K.fx * qx[q]) / qz[q]) + K.cx) + 0.5f);
-            const float v = floorf((((K.fy * qy[q]) / qz[q]) + K.cy) + 0.5f);
-            if (u >= 0.0f && u < (float)W && v >= 0.0f && v < (float)H) {
-                j[q] = (int)v * W + (int)u;
-                fu[q] = u;
-                fv[q] = v;
+    for (int k = 0; k < 12; ++k) T[k] = T32[p * 12 + k];
+
+    double acc[kNeq];
+#pragma unroll
+    for (int k = 0; k < kNeq; ++k) acc[k] = 0.0;
+
+    const int start = b * chunk;
+    const int end = min(start + chunk, N);
+    int32_t* arow = kAssoc ? assoc + (size_t)p * N : nullptr;
+    for (int i = start + threadIdx.x * 4; i < end; i += kRedStep) {
+        const short4 d4 = load_depth4<kAligned>(sD, i, end);
+        const int dd[4] = {d4.x, d4.y, d4.z, d4.w};
+        const int v0 = i / W;
+        const int u0 = i - v0 * W;
+        // spec a7: P' = R P + t (fixed order, no FMA); projective association
+        float qx[4], qy[4], qz[4], fu[4], fv[4];
+        int j[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            int u = u0 + q, v = v0;
+            if (u >= W) {
+                u -= W;
+                ++v;
             }
+            float sx, sy, sz;
+            backproject<kFast>((i + q) < end ? dd[q] : 0, u, v, K, F, sx, sy, sz);
+            qx[q] = ((T[0] * sx + T[1] * sy) + T[2] * sz) + T[3];
+            qy[q] = ((T[4] * sx + T[5] * sy) + T[6] * sz) + T[7];
+            qz[q] = ((T[8] * sx + T[9] * sy) + T[10] * sz) + T[11];
+            const bool vz = sz > 0.0f && qz[q] > 0.0f;
+            const float qzs = vz ? qz[q] : 1.0f;
+            const float uu = floorf((((K.fx * qx[q]) / qzs) + K.cx) + 0.5f);
+            const float vv = floorf((((K.fy * qy[q]) / qzs) + K.cy) + 0.5f);
+            const bool in = vz && uu >= 0.0f && uu < (float)W && vv >= 0.0f && vv < (float)H;
+            fu[q] = in ? uu : 0.0f;
+            fv[q] = in ? vv : 0.0f;
+            j[q] = in ? (int)fv[q] * W + (int)fu[q] : -1;
+        }
+        // four 16-byte fetches back to back (clamped index: no branch)
+        float4 t[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t[q] = rec[j[q] >= 0 ? j[q] : 0];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float tz = t[q].x;
+            const float tx = bp_div<kFast>((fu[q] - K.cx) * tz, K.fx, F.rfx);
+            const float ty = bp_div<kFast>((fv[q] - K.cy) * tz, K.fy, F.rfy);
+            const float nx = t[q].y, ny = t[q].z, nz = t[q].w;
+            const float dx = qx[q] - tx, dy = qy[q] - ty, dz = qz[q] - tz;
+            const float d2 = (dx * dx + dy * dy) + dz * dz;
+            const bool nvalid = !(nx == 0.0f && ny == 0.0f && nz == 0.0f);
+            const bool ok = j[q] >= 0 && tz > 0.0f && nvalid && d2 < thr2;
+            if (kAssoc && (i + q) < end) arow[i + q] = ok ? j[q] : -1;
+            // spec a8: r = n.(P' - P_t); J = [P' x n, n]  (zeros when unmatched)
+            const float n0 = ok ? nx : 0.0f, n1 = ok ? ny : 0.0f, n2 = ok ? nz : 0.0f;
+            const float r = ok ? (nx * dx + ny * dy) + nz * dz : 0.0f;
+            float Jf[6];
+            Jf[0] = qy[q] * n2 - qz[q] * n1;
+            Jf[1] = qz[q] * n0 - qx[q] * n2;
+            Jf[2] = qx[q] * n1 - qy[q] * n0;
+            Jf[3] = n0;
+            Jf[4] = n1;
+            Jf[5] = n2;
+            // spec a9: fp32 products are exact in fp64; one rounding per add
+            int k = 0;
+#pragma unroll
+            for (int a = 0; a < 6; ++a)
+#pragma unroll
+                for (int bb = a; bb < 6; ++bb) {
+                    acc[k] = fma((double)Jf[a], (double)Jf[bb], acc[k]);
+                    ++k;
+                }
+#pragma unroll
+            for (int a = 0; a < 6; ++a) acc[21 + a] = fma((double)Jf[a], (double)r, acc[21 + a]);
+            acc[27] = fma((double)r, (double)r, acc[27]);
+            acc[28] += ok ? 1.0 : 0.0;
         }
     }
-    // all four fetches issued back to back from clamped indices (no branch)
-    float4 t[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) t[q] = rec[j[q] >= 0 ? j[q] : 0];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const float tz = t[q].x;
-        const float tx = ((fu[q] - K.cx) * tz) / K.fx;  // = k_prep's X of pixel (u', v')
-        const float ty = ((fv[q] - K.cy) * tz) / K.fy;
-        const float nx = t[q].y, ny = t[q].z, nz = t[q].w;
-        const float dx = qx[q] - tx, dy = qy[q] - ty, dz = qz[q] - tz;
-        const float d2 = (dx * dx + dy * dy) + dz * dz;
-        const bool nvalid = !(nx == 0.0f && ny == 0.0f && nz == 0.0f);
-        const bool ok = j[q] >= 0 && tz > 0.0f && nvalid && d2 < thr2;
-        if (kAssoc && (i + q) < end) arow[i + q] = ok ? j[q] : -1;
-        // spec a8: r = n.(P' - P_t); J = [P' x n, n]  (zeros when unmatched)
-        const float n0 = ok ? nx : 0.0f, n1 = ok ? ny : 0.0f, n2 = ok ? nz : 0.0f;
-        const float r = ok ? (nx * dx + ny * dy) + nz * dz : 0.0f;
-        float Jf[6];
-        Jf[0] = qy[q] * n2 - qz[q] * n1;
-        Jf[1] = qz[q] * n0 - qx[q] * n2;
-        Jf[2] = qx[q] * n1 - qy[q] * n0;
-        Jf[3] = n0;
-        Jf[4] = n1;
-        Jf[5] = n2;
-        // spec a9: fp32 products are exact in fp64; one rounding per add
-        int k = 0;
-#pragma unroll
-        for (int a = 0; a < 6; ++a)
-#pragma unroll
-            for (int b = a; b < 6; ++b) {
-                acc_fma<double>(acc[k], Jf[a], Jf[b]);
-                ++k;
-            }
-#pragma unroll
-        for (int a = 0; a < 6; ++a) acc_fma<double>(acc[21 + a], Jf[a], r);
-        acc_fma<double>(acc[27], r, r);
-        acc[28] += ok ? 1.0 : 0.0;
-    }
-}
 
-// Wave butterfly (lane-symmetric: every lane ends with the same sum), then
-// waves in fixed order through LDS; one 29-double partial per workgroup.
-__device__ __forceinline__ void block_reduce_store(double* acc, double (*red)[kNeq],
-                                                   double* __restrict__ out)
-{
+    // wave butterfly (lane-symmetric: every lane ends with the same sum),
+    // then the four waves in fixed order through LDS
 #pragma unroll
     for (int k = 0; k < kNeq; ++k) {
         double v = acc[k];
@@ -294,50 +348,9 @@ __device__ __forceinline__ void block_reduce_store(double* acc, double (*red)[kN
         double s = red[0][k];
 #pragma unroll
         for (int w = 1; w < kRedThreads / 64; ++w) s += red[w][k];
-        out[k] = s;
+        partials[((size_t)p * gridDim.x + b) * kNeq + k] = s;
     }
 }
-
-// grid (nblk, n_pairs); workgroup b of pair p covers pixels
-// [b*chunk, min((b+1)*chunk, N)); chunk is a multiple of kRedStep.
-template <bool kAssoc>
-__global__ __launch_bounds__(kRedThreads) void k_reduce(
-    const float* __restrict__ xyz, const float4* __restrict__ recs, size_t P, PairMap pm,
-    const float* __restrict__ T32, int W, int H, Intr K, float thr2, int chunk,
-    double* __restrict__ partials, int32_t* __restrict__ assoc)
-{
-    __shared__ double red[kRedThreads / 64][kNeq];
-    const int p = blockIdx.y;
-    const int b = blockIdx.x;
-    const int N = W * H;
-    const float* sX = xyz + (size_t)(pm.src0 + p) * 3 * P;
-    const float* sY = sX + P;
-    const float* sZ = sY + P;
-    const float4* rec = recs + (size_t)(pm.tgt0 + p) * P;
-    float T[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) T[k] = T32[p * 12 + k];
-
-    double acc[kNeq];
-#pragma unroll
-    for (int k = 0; k < kNeq; ++k) acc[k] = 0.0;
-
-    const int start = b * chunk;
-    const int end = min(start + chunk, N);
-    int32_t* arow = kAssoc ? assoc + (size_t)p * N : nullptr;
-    for (int i = start + threadIdx.x * 4; i < end; i += kRedStep) {
-        // i % 4 == 0 and P >= N + 4: the float4 never leaves the zeroed pad
-        const float4 x4 = *reinterpret_cast<const float4*>(sX + i);
-        const float4 y4 = *reinterpret_cast<const float4*>(sY + i);
-        const float4 z4 = *reinterpret_cast<const float4*>(sZ + i);
-        const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
-        const float ys[4] = {y4.x, y4.y, y4.z, y4.w};
-        const float zs[4] = {z4.x, z4.y, z4.z, z4.w};
-        process4<kAssoc>(xs, ys, zs, i, end, T, K, W, H, thr2, rec, acc, arow);
-    }
-    block_reduce_store(acc, red, partials + ((size_t)p * gridDim.x + b) * kNeq);
-}
-
 
 // ----------------------------------------------------------------- k_solve --
 // LDL^T + SE(3) exp, same algorithm and evaluation order as oracle_solve /
@@ -561,12 +574,14 @@ struct youth_icp_ctx {
     size_t P = 0;
     int max_frames = 0;
     Intr K{};
+    FastK F{};
+    bool fast = false;  // verified 3-op back-projection division
     youth_icp_params prm{};
     hipStream_t stream = nullptr;
 
     int16_t* d_depth = nullptr;  // [max_frames][N] staging for host-side APIs
-    float* d_xyz = nullptr;      // [max_frames][3][P]
     float4* d_rec = nullptr;     // [max_frames][P] target records {z, nx, ny, nz}
+    float* d_xyz = nullptr;      // [max_frames][3][P] (lazy: stage-level API only)
     double* d_T64 = nullptr;     // [max_frames][16]
     float* d_T32 = nullptr;      // [max_frames][12]
     int32_t* d_status = nullptr; // [max_frames]
@@ -578,6 +593,7 @@ struct youth_icp_ctx {
     double* d_neq = nullptr;  // [max_frames][29]
     int32_t* d_assoc = nullptr;
     float* d_Tout = nullptr;  // [max_frames][16]
+    unsigned* d_flag = nullptr;
 
     int last_pairs = 0;
     int last_iters = 0;
@@ -594,7 +610,8 @@ struct youth_icp_ctx {
 
 static int reduce_geometry(const youth_icp_ctx* c, int n_pairs, int* chunk_out)
 {
-    // ~2048 workgroups in flight over the batch, at least 8 px per lane.
+    // ~2048 workgroups per launch (tools/kbench: best of 1024/2048/4096 at
+    // 64 pairs), at least 8 pixels per lane.
     const int target_blocks = 2048;
     int nb = (target_blocks + n_pairs - 1) / n_pairs;
     const int max_nb = (c->N + 2 * kRedStep - 1) / (2 * kRedStep);
@@ -632,6 +649,15 @@ static int ensure_assoc(youth_icp_ctx* c)
 {
     if (c->d_assoc) return YOUTH_OK;
     HIP_TRY(hipMalloc(&c->d_assoc, (size_t)c->max_frames * c->N * sizeof(int32_t)));
+    return YOUTH_OK;
+}
+
+static int ensure_xyz(youth_icp_ctx* c)
+{
+    if (c->d_xyz) return YOUTH_OK;
+    const size_t bytes = 3 * c->P * sizeof(float) * (size_t)c->max_frames;
+    HIP_TRY(hipMalloc(&c->d_xyz, bytes));
+    HIP_TRY(hipMemset(c->d_xyz, 0, bytes));
     return YOUTH_OK;
 }
 
@@ -673,51 +699,75 @@ static int ev_harvest(youth_icp_ctx* c)
     return YOUTH_OK;
 }
 
-// Launch k_prep for frames [out0, out0 + n_frames).
-static int launch_prep(youth_icp_ctx* c, hipStream_t s, const int16_t* da, const int16_t* db,
-                       int n_a, int out0, int n_frames, int rec_first, int xyz_end)
+// Target records (and optionally XYZ planes) for n_frames depth frames at
+// `depth`, into workspace frames [out0, out0 + n_frames).
+static int launch_prep(youth_icp_ctx* c, hipStream_t s, const int16_t* depth, int n_frames,
+                       int out0, bool want_xyz)
 {
     if (n_frames <= 0) return YOUTH_OK;
+    if (want_xyz) {
+        int rc = ensure_xyz(c);
+        if (rc) return rc;
+    }
     dim3 grid((c->W + kTileW - 1) / kTileW, (c->H + kTileH - 1) / kTileH, n_frames);
     EventPair ep{};
     int rc = ev_begin(c, s, &ep, 2);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_prep, grid, dim3(kPrepThreads), 0, s, da, db, n_a, out0, rec_first,
-                       xyz_end, c->W, c->H, c->P, c->K, c->d_xyz, c->d_rec);
+    float* xyz = want_xyz ? c->d_xyz : nullptr;
+    if (c->fast)
+        hipLaunchKernelGGL(k_prep<true>, grid, dim3(kPrepThreads), 0, s, depth, out0, c->W, c->H,
+                           c->P, c->K, c->F, c->d_rec, xyz);
+    else
+        hipLaunchKernelGGL(k_prep<false>, grid, dim3(kPrepThreads), 0, s, depth, out0, c->W, c->H,
+                           c->P, c->K, c->F, c->d_rec, xyz);
     HIP_TRY(hipGetLastError());
     return ev_end(c, s, &ep);
 }
 
-static int launch_reduce(youth_icp_ctx* c, hipStream_t s, PairMap pm, int n_pairs,
-                         bool assoc, int* nblk_out)
+template <bool kAssoc, bool kFast, bool kAligned>
+static void launch_reduce_t(youth_icp_ctx* c, hipStream_t s, dim3 grid, const int16_t* dsrc,
+                            PairMap pm, float thr2, int chunk)
+{
+    hipLaunchKernelGGL((k_reduce<kAssoc, kFast, kAligned>), grid, dim3(kRedThreads), 0, s, dsrc,
+                       c->d_rec, c->P, pm, c->d_T32, c->W, c->H, c->K, c->F, thr2, chunk,
+                       c->d_partials, kAssoc ? c->d_assoc : (int32_t*)nullptr);
+}
+
+static int launch_reduce(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, PairMap pm,
+                         int n_pairs, bool assoc, int* nblk_out)
 {
     int chunk = 0;
     const int nb = reduce_geometry(c, n_pairs, &chunk);
     int rc = ensure_partials(c, (size_t)nb * n_pairs * kNeq);
     if (rc) return rc;
+    if (assoc) {
+        rc = ensure_assoc(c);
+        if (rc) return rc;
+    }
     const float thr2 = c->prm.dist_thresh * c->prm.dist_thresh;
+    const bool aligned = (reinterpret_cast<uintptr_t>(dsrc) % 8 == 0) && (c->N % 4 == 0);
     dim3 grid(nb, n_pairs);
     EventPair ep{};
     rc = ev_begin(c, s, &ep, 0);
     if (rc) return rc;
-    if (assoc) {
-        rc = ensure_assoc(c);
-        if (rc) return rc;
-        hipLaunchKernelGGL(k_reduce<true>, grid, dim3(kRedThreads), 0, s, c->d_xyz, c->d_rec,
-                           c->P, pm, c->d_T32, c->W, c->H, c->K, thr2, chunk, c->d_partials,
-                           c->d_assoc);
-    } else {
-        hipLaunchKernelGGL(k_reduce<false>, grid, dim3(kRedThreads), 0, s, c->d_xyz, c->d_rec,
-                           c->P, pm, c->d_T32, c->W, c->H, c->K, thr2, chunk, c->d_partials,
-                           (int32_t*)nullptr);
+    const int sel = (assoc ? 4 : 0) | (c->fast ? 2 : 0) | (aligned ? 1 : 0);
+    switch (sel) {
+    case 0: launch_reduce_t<false, false, false>(c, s, grid, dsrc, pm, thr2, chunk); break;
+    case 1: launch_reduce_t<false, false, true>(c, s, grid, dsrc, pm, thr2, chunk); break;
+    case 2: launch_reduce_t<false, true, false>(c, s, grid, dsrc, pm, thr2, chunk); break;
+    case 3: launch_reduce_t<false, true, true>(c, s, grid, dsrc, pm, thr2, chunk); break;
+    case 4: launch_reduce_t<true, false, false>(c, s, grid, dsrc, pm, thr2, chunk); break;
+    case 5: launch_reduce_t<true, false, true>(c, s, grid, dsrc, pm, thr2, chunk); break;
+    case 6: launch_reduce_t<true, true, false>(c, s, grid, dsrc, pm, thr2, chunk); break;
+    default: launch_reduce_t<true, true, true>(c, s, grid, dsrc, pm, thr2, chunk); break;
     }
     HIP_TRY(hipGetLastError());
     *nblk_out = nb;
     return ev_end(c, s, &ep);
 }
 
-static int run_iterations(youth_icp_ctx* c, hipStream_t s, PairMap pm, int n_pairs,
-                          const double* T_init_host)
+static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, PairMap pm,
+                          int n_pairs, const double* T_init_host)
 {
     const int iters = c->prm.iters;
     int rc = ensure_stats(c, iters > 0 ? iters : 1);
@@ -733,7 +783,7 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, PairMap pm, int n_pai
     HIP_TRY(hipGetLastError());
     for (int it = 0; it < iters; ++it) {
         int nb = 0;
-        rc = launch_reduce(c, s, pm, n_pairs, false, &nb);
+        rc = launch_reduce(c, s, dsrc, pm, n_pairs, false, &nb);
         if (rc) return rc;
         EventPair ep{};
         rc = ev_begin(c, s, &ep, 1);
@@ -770,6 +820,23 @@ static int bind_device(youth_icp_ctx* c)
     return YOUTH_OK;
 }
 
+// Decide the division path for these intrinsics (k_verify_fastdiv).
+static int verify_fastdiv(youth_icp_ctx* c)
+{
+    c->fast = false;
+    const char* off = getenv("YOUTH_ICP_NO_FASTDIV");
+    if (off && *off && *off != '0') return YOUTH_OK;
+    HIP_TRY(hipMemsetAsync(c->d_flag, 0, sizeof(unsigned), c->stream));
+    hipLaunchKernelGGL(k_verify_fastdiv, dim3(128, 64), dim3(256), 0, c->stream, c->K, c->F, c->W,
+                       c->H, c->d_flag);
+    HIP_TRY(hipGetLastError());
+    unsigned bad = 1;
+    HIP_TRY(hipMemcpyAsync(&bad, c->d_flag, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->fast = bad == 0;
+    return YOUTH_OK;
+}
+
 extern "C" {
 
 youth_intrinsics youth_default_intrinsics(int width, int height)
@@ -800,6 +867,8 @@ int youth_icp_device_count(void)
     return n;
 }
 
+int youth_icp_fastdiv_enabled(youth_icp_ctx* c) { return c && c->fast ? 1 : 0; }
+
 void youth_icp_destroy(youth_icp_ctx* c)
 {
     if (!c) return;
@@ -811,8 +880,9 @@ void youth_icp_destroy(youth_icp_ctx* c)
             (void)hipEventDestroy(e.a);
             (void)hipEventDestroy(e.b);
         }
-    void* bufs[] = {c->d_depth, c->d_xyz,   c->d_rec,      c->d_T64, c->d_T32,   c->d_status,
-                    c->d_Tinit, c->d_stats, c->d_partials, c->d_neq, c->d_assoc, c->d_Tout};
+    void* bufs[] = {c->d_depth, c->d_rec,   c->d_xyz,      c->d_T64, c->d_T32,   c->d_status,
+                    c->d_Tinit, c->d_stats, c->d_partials, c->d_neq, c->d_assoc, c->d_Tout,
+                    c->d_flag};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -823,10 +893,10 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
                                 const youth_intrinsics* K, const youth_icp_params* P)
 {
     if (W < 3 || H < 3 || max_frames < 2 || (long long)W * H > (1LL << 30)) {
-        set_error(YOUTH_EINVAL, "youth_icp_create: bad size %d", W);
+        set_error(YOUTH_EINVAL, "youth_icp_create: bad size %dx%d", W, H);
         return nullptr;
     }
-    int ndev = youth_icp_device_count();
+    const int ndev = youth_icp_device_count();
     if (ndev <= 0 || device < 0 || device >= ndev) {
         set_error(YOUTH_ENODEV, "youth_icp_create: no HIP device %d", device);
         return nullptr;
@@ -840,6 +910,7 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
     c->max_frames = max_frames;
     const youth_intrinsics Kd = K ? *K : youth_default_intrinsics(W, H);
     c->K = Intr{Kd.fx, Kd.fy, Kd.cx, Kd.cy, Kd.depth_scale};
+    c->F = FastK{1.0f / Kd.fx, 1.0f / Kd.fy, 1.0f / Kd.depth_scale};
     c->prm = P ? *P : youth_default_params();
     auto fail = [&](const char* what, hipError_t e) -> youth_icp_ctx* {
         set_error(YOUTH_EHIP, "youth_icp_create: %s (%d)", what, (int)e);
@@ -851,14 +922,11 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess)
         return fail("hipStreamCreate", e);
     const size_t MF = (size_t)max_frames;
-    const size_t plane_bytes = 3 * c->P * sizeof(float) * MF;
     const size_t rec_bytes = c->P * sizeof(float4) * MF;
     if ((e = hipMalloc(&c->d_depth, MF * c->N * sizeof(int16_t))) != hipSuccess)
         return fail("hipMalloc depth", e);
-    if ((e = hipMalloc(&c->d_xyz, plane_bytes)) != hipSuccess) return fail("hipMalloc xyz", e);
     if ((e = hipMalloc(&c->d_rec, rec_bytes)) != hipSuccess) return fail("hipMalloc rec", e);
-    // the pad beyond N of every plane must read as an invalid point (Z = 0)
-    if ((e = hipMemset(c->d_xyz, 0, plane_bytes)) != hipSuccess) return fail("memset xyz", e);
+    // the pad beyond N of every frame must read as an invalid point (z = 0)
     if ((e = hipMemset(c->d_rec, 0, rec_bytes)) != hipSuccess) return fail("memset rec", e);
     if ((e = hipMalloc(&c->d_T64, MF * 16 * sizeof(double))) != hipSuccess)
         return fail("hipMalloc T64", e);
@@ -872,8 +940,10 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         return fail("hipMalloc neq", e);
     if ((e = hipMalloc(&c->d_Tout, MF * 16 * sizeof(float))) != hipSuccess)
         return fail("hipMalloc Tout", e);
+    if ((e = hipMalloc(&c->d_flag, 16)) != hipSuccess) return fail("hipMalloc flag", e);
     if ((e = hipDeviceSynchronize()) != hipSuccess) return fail("sync", e);
-    if (ensure_stats(c, c->prm.iters > 0 ? c->prm.iters : 1) != YOUTH_OK) {
+    if (ensure_stats(c, c->prm.iters > 0 ? c->prm.iters : 1) != YOUTH_OK ||
+        verify_fastdiv(c) != YOUTH_OK) {
         youth_icp_destroy(c);
         return nullptr;
     }
@@ -884,15 +954,15 @@ int youth_icp_align_pairs_device(youth_icp_ctx* c, const int16_t* d_src, const i
                                  int n_pairs, const double* T_init, float* d_T_out,
                                  void* stream)
 {
-    if (!c || !d_src || !d_dst || n_pairs <= 0 || 2 * n_pairs > c->max_frames)
+    if (!c || !d_src || !d_dst || n_pairs <= 0 || n_pairs > c->max_frames)
         return set_error(YOUTH_EINVAL, "align_pairs: bad arguments %d", n_pairs);
     int rc = bind_device(c);
     if (rc) return rc;
     hipStream_t s = pick_stream(c, stream);
-    // frames [0, n): sources (XYZ only); [n, 2n): targets (XYZ + normals)
-    rc = launch_prep(c, s, d_src, d_dst, n_pairs, 0, 2 * n_pairs, n_pairs, n_pairs);
+    // targets -> records [0, n); sources are read from d_src by k_reduce
+    rc = launch_prep(c, s, d_dst, n_pairs, 0, false);
     if (rc) return rc;
-    rc = run_iterations(c, s, PairMap{0, n_pairs}, n_pairs, T_init);
+    rc = run_iterations(c, s, d_src, PairMap{0, 0}, n_pairs, T_init);
     if (rc) return rc;
     return export_poses(c, s, n_pairs, d_T_out);
 }
@@ -900,15 +970,16 @@ int youth_icp_align_pairs_device(youth_icp_ctx* c, const int16_t* d_src, const i
 int youth_icp_align_sequence_device(youth_icp_ctx* c, const int16_t* d_frames, int n_frames,
                                     float* d_T_out, void* stream)
 {
-    if (!c || !d_frames || n_frames < 2 || n_frames > c->max_frames)
+    if (!c || !d_frames || n_frames < 2 || n_frames - 1 > c->max_frames)
         return set_error(YOUTH_EINVAL, "align_sequence: bad arguments %d", n_frames);
     int rc = bind_device(c);
     if (rc) return rc;
     hipStream_t s = pick_stream(c, stream);
-    rc = launch_prep(c, s, d_frames, d_frames, n_frames, 0, n_frames, 0, n_frames);
+    // every frame but the last is a target: one record set per frame, reused
+    rc = launch_prep(c, s, d_frames, n_frames - 1, 0, false);
     if (rc) return rc;
-    // pair k: source frame k+1, target frame k
-    rc = run_iterations(c, s, PairMap{1, 0}, n_frames - 1, nullptr);
+    // pair k: source depth frame k+1, target record frame k
+    rc = run_iterations(c, s, d_frames, PairMap{1, 0}, n_frames - 1, nullptr);
     if (rc) return rc;
     return export_poses(c, s, n_frames - 1, d_T_out);
 }
@@ -1002,8 +1073,7 @@ int youth_icp_prepare_host(youth_icp_ctx* c, const int16_t* depth, int n_frames,
     const size_t N = c->N;
     HIP_TRY(hipMemcpyAsync(c->d_depth, depth, (size_t)n_frames * N * sizeof(int16_t),
                            hipMemcpyHostToDevice, s));
-    rc = launch_prep(c, s, c->d_depth, c->d_depth, n_frames, 0, n_frames,
-                     want_normals ? 0 : n_frames, n_frames);
+    rc = launch_prep(c, s, c->d_depth, n_frames, 0, true);
     if (rc) return rc;
     float* outs[6] = {X, Y, Z, NX, NY, NZ};
     for (int f = 0; f < n_frames; ++f)
@@ -1014,9 +1084,10 @@ int youth_icp_prepare_host(youth_icp_ctx* c, const int16_t* depth, int n_frames,
                 const float* base = c->d_xyz + (size_t)f * 3 * c->P + (size_t)k * c->P;
                 HIP_TRY(hipMemcpyAsync(dst, base, N * sizeof(float), hipMemcpyDeviceToHost, s));
             } else {  // component k-2 of the {z, nx, ny, nz} records
-                const float* base = reinterpret_cast<const float*>(c->d_rec + (size_t)f * c->P) + (k - 2);
-                HIP_TRY(hipMemcpy2DAsync(dst, sizeof(float), base, sizeof(float4), sizeof(float), N,
-                                         hipMemcpyDeviceToHost, s));
+                const float* base = reinterpret_cast<const float*>(c->d_rec + (size_t)f * c->P) +
+                                    (k - 2);
+                HIP_TRY(hipMemcpy2DAsync(dst, sizeof(float), base, sizeof(float4), sizeof(float),
+                                         N, hipMemcpyDeviceToHost, s));
             }
         }
     HIP_TRY(hipStreamSynchronize(s));
@@ -1026,19 +1097,18 @@ int youth_icp_prepare_host(youth_icp_ctx* c, const int16_t* depth, int n_frames,
 int youth_icp_reduce_host(youth_icp_ctx* c, const int16_t* src, const int16_t* dst,
                           const float* T12, int32_t* assoc, double* neq)
 {
-    if (!c || !src || !dst || !T12)
-        return set_error(YOUTH_EINVAL, "reduce_host: bad arguments");
+    if (!c || !src || !dst || !T12) return set_error(YOUTH_EINVAL, "reduce_host: bad arguments");
     int rc = bind_device(c);
     if (rc) return rc;
     hipStream_t s = c->stream;
     const size_t N = c->N;
     HIP_TRY(hipMemcpyAsync(c->d_depth, src, N * sizeof(int16_t), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(c->d_depth + N, dst, N * sizeof(int16_t), hipMemcpyHostToDevice, s));
-    rc = launch_prep(c, s, c->d_depth, c->d_depth, 2, 0, 2, 1, 1);
+    rc = launch_prep(c, s, c->d_depth + N, 1, 1, false);  // target -> record frame 1
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(c->d_T32, T12, 12 * sizeof(float), hipMemcpyHostToDevice, s));
     int nb = 0;
-    rc = launch_reduce(c, s, PairMap{0, 1}, 1, assoc != nullptr, &nb);
+    rc = launch_reduce(c, s, c->d_depth, PairMap{0, 1}, 1, assoc != nullptr, &nb);
     if (rc) return rc;
     hipLaunchKernelGGL(k_solve, dim3(1), dim3(64), 0, s, c->d_partials, nb, 0, 1, c->d_T64,
                        c->d_T32, c->d_status, (double*)nullptr, c->d_neq);
@@ -1091,7 +1161,9 @@ int youth_icp_align_batch(const int16_t* src, const int16_t* dst, int n_pairs, i
         if (c) youth_icp_destroy(c);
         g_batch_ctx = nullptr;
         c = youth_icp_create(0, W, H, 2 * n_pairs, &Kd, &P);
-        if (!c) return g_last_error.find("no HIP device") != std::string::npos ? YOUTH_ENODEV : YOUTH_EHIP;
+        if (!c)
+            return g_last_error.find("no HIP device") != std::string::npos ? YOUTH_ENODEV
+                                                                          : YOUTH_EHIP;
         g_batch_ctx = c;
     }
     c->prm = P;
@@ -1099,16 +1171,17 @@ int youth_icp_align_batch(const int16_t* src, const int16_t* dst, int n_pairs, i
     if (rc) return rc;
     hipStream_t s = c->stream;
     const size_t N = c->N;
-    HIP_TRY(hipMemcpyAsync(c->d_depth, src, (size_t)n_pairs * N * sizeof(int16_t),
-                           hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(c->d_depth + (size_t)n_pairs * N, dst,
-                           (size_t)n_pairs * N * sizeof(int16_t), hipMemcpyHostToDevice, s));
-    rc = youth_icp_align_pairs_device(c, c->d_depth, c->d_depth + (size_t)n_pairs * N, n_pairs,
-                                      nullptr, c->d_Tout, s);
+    int16_t* d_s = c->d_depth;
+    int16_t* d_d = c->d_depth + (size_t)n_pairs * N;
+    HIP_TRY(hipMemcpyAsync(d_s, src, (size_t)n_pairs * N * sizeof(int16_t), hipMemcpyHostToDevice,
+                           s));
+    HIP_TRY(hipMemcpyAsync(d_d, dst, (size_t)n_pairs * N * sizeof(int16_t), hipMemcpyHostToDevice,
+                           s));
+    rc = youth_icp_align_pairs_device(c, d_s, d_d, n_pairs, nullptr, c->d_Tout, s);
     if (rc) return rc;
     if (assoc_out) {
         int nb = 0;
-        rc = launch_reduce(c, s, PairMap{0, n_pairs}, n_pairs, true, &nb);
+        rc = launch_reduce(c, s, d_s, PairMap{0, 0}, n_pairs, true, &nb);
         if (rc) return rc;
         HIP_TRY(hipMemcpyAsync(assoc_out, c->d_assoc, (size_t)n_pairs * N * sizeof(int32_t),
                                hipMemcpyDeviceToHost, s));
@@ -1131,13 +1204,15 @@ int youth_icp_track_frame(youth_icp_ctx* c, const int16_t* depth, const double* 
     const int slot = c->track_ref == 0 ? 1 : 0;
     HIP_TRY(hipMemcpyAsync(c->d_depth + (size_t)slot * N, depth, N * sizeof(int16_t),
                            hipMemcpyHostToDevice, s));
-    rc = launch_prep(c, s, c->d_depth + (size_t)slot * N, nullptr, 1, slot, 1, 0, 1);
+    // the new frame is the next call's target: its records go to `slot`
+    rc = launch_prep(c, s, c->d_depth + (size_t)slot * N, 1, slot, false);
     if (rc) return rc;
     int32_t st = 0;
     const int ref = c->track_ref;
     if (has_ref) *has_ref = ref >= 0;
     if (ref >= 0) {
-        rc = run_iterations(c, s, PairMap{slot, ref}, 1, T_init);
+        // source: the new frame's depth (staging slot); target: ref's records
+        rc = run_iterations(c, s, c->d_depth + (size_t)slot * N, PairMap{0, ref}, 1, T_init);
         if (rc) return rc;
         HIP_TRY(hipMemcpyAsync(T_rel, c->d_T64, 16 * sizeof(double), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(&st, c->d_status, sizeof(int32_t), hipMemcpyDeviceToHost, s));
@@ -1145,6 +1220,11 @@ int youth_icp_track_frame(youth_icp_ctx* c, const int16_t* depth, const double* 
     HIP_TRY(hipStreamSynchronize(s));
     if (ref < 0) {
         for (int i = 0; i < 16; ++i) T_rel[i] = (i % 5) == 0 ? 1.0 : 0.0;
+    } else {
+        T_rel[12] = 0.0;
+        T_rel[13] = 0.0;
+        T_rel[14] = 0.0;
+        T_rel[15] = 1.0;
     }
     c->track_ref = slot;
     return st;

@@ -82,6 +82,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "youth_default_params": (Params, []),
         "youth_icp_last_error": (c_char_p, []),
         "youth_icp_device_count": (c_int, []),
+        "youth_icp_fastdiv_enabled": (c_int, [c_void_p]),
         "youth_icp_align_batch": (c_int, [P16, P16, c_int, c_int, c_int, POINTER(Intrinsics),
                                           c_int, PF, PI32]),
         "youth_icp_create": (c_void_p, [c_int, c_int, c_int, c_int, POINTER(Intrinsics),
@@ -275,6 +276,11 @@ class IcpContext:
     @property
     def handle(self) -> int:
         return self._ctx
+
+    @property
+    def fastdiv(self) -> bool:
+        """True when the verified 3-op back-projection division is in use."""
+        return bool(self._lib.youth_icp_fastdiv_enabled(self._ctx))
 
     def close(self):
         if getattr(self, "_ctx", None):

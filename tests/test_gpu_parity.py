@@ -49,7 +49,7 @@ def test_backproject_kat_on_gpu():
         with youth_icp.IcpContext(W, H, 2) as ctx:
             X, Y, Z, *_ = ctx.prepare(depth, want_normals=False)
         for _, _, u, v, d, xb, yb, zb in rows:
-            got = (int(_bits(X[0, v, u])), int(_bits(Y[0, v, u])), int(_bits(Z[0, v, u])))
+            got = tuple(int(_bits(A[0, v, u]).item()) for A in (X, Y, Z))
             assert got == (xb, yb, zb), (W, H, u, v, d)
 
 
@@ -301,3 +301,42 @@ def test_algorithm_module_thread_entry():
     youth_icp.stopSlamModule()
     t.join(timeout=10)
     assert not t.is_alive()
+
+
+# ------------------------------------------------ division path / alignment --
+def test_fastdiv_path_is_bit_identical_to_ieee(monkeypatch):
+    """The verified 3-op back-projection divide must change nothing: both
+    paths give the same association and bit-identical poses."""
+    src, dst, _ = youth_synth.pairs(30, 3)
+    import torch
+    ds = torch.from_numpy(src).cuda()
+    dd = torch.from_numpy(dst).cuda()
+    torch.cuda.synchronize()
+    out = {}
+    for mode in ("fast", "ieee"):
+        if mode == "ieee":
+            monkeypatch.setenv("YOUTH_ICP_NO_FASTDIV", "1")
+        with youth_icp.IcpContext(640, 480, 3) as ctx:
+            assert ctx.fastdiv == (mode == "fast")
+            ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), 3)
+            out[mode] = ctx.get_poses(3)[0]
+            a, _ = ctx.reduce(src[0], dst[0], out[mode][0][:3].astype(np.float32))
+            out[mode + "_assoc"] = a
+    assert np.array_equal(out["fast"], out["ieee"])
+    assert np.array_equal(out["fast_assoc"], out["ieee_assoc"])
+
+
+def test_unaligned_source_pointer():
+    """Source frames at an odd int16 offset take the unaligned depth path."""
+    src, dst, _ = youth_synth.pairs(31, 2, 160, 120)
+    import torch
+    flat = torch.zeros(src.size + 1, dtype=torch.int16, device="cuda")
+    flat[1:] = torch.from_numpy(src.reshape(-1)).cuda()
+    dd = torch.from_numpy(dst).cuda()
+    torch.cuda.synchronize()
+    with youth_icp.IcpContext(160, 120, 2) as ctx:
+        ctx.align_pairs_device(flat.data_ptr() + 2, dd.data_ptr(), 2)
+        T64, _, st = ctx.get_poses(2)
+    for p in range(2):
+        To, _, sto, _ = oracle.align(src[p], dst[p])
+        assert st[p] == sto and _pose_err(T64[p], To) <= POSE_TOL

@@ -68,52 +68,58 @@ int main(int argc, char** argv)
         fprintf(stderr, "align: %s\n", youth_icp_last_error());
         return 1;
     }
-    // every frame gets XYZ planes (the old variants read target planes too)
-    if (launch_prep(c, c->stream, d_src, d_dst, n, 0, 2 * n, n, 2 * n) != 0) return 1;
+    // XYZ planes for every frame (the v0 reference reads SoA planes); sources
+    // -> workspace frames [0, n), targets -> [n, 2n) (records + planes)
+    if (launch_prep(c, c->stream, d_src, n, 0, true) != 0) return 1;
+    if (launch_prep(c, c->stream, d_dst, n, n, true) != 0) return 1;
     float* d_nrm;
     CK(hipMalloc(&d_nrm, (size_t)2 * n * 3 * c->P * sizeof(float)));
     CK(hipMemset(d_nrm, 0, (size_t)2 * n * 3 * c->P * sizeof(float)));
     hipLaunchKernelGGL(k_unpack_normals, dim3((N + 255) / 256, 2 * n), dim3(256), 0, c->stream,
                        c->d_rec, c->P, N, d_nrm);
-    float4* d_rec32;
-    CK(hipMalloc(&d_rec32, (size_t)2 * n * c->P * 2 * sizeof(float4)));
-    hipLaunchKernelGGL(k_pack_records32, dim3((N + 255) / 256, 2 * n), dim3(256), 0, c->stream,
-                       c->d_xyz, d_nrm, c->P, N, d_rec32);
+    float* d_big;  // streaming-calibration buffer: 28 B/px x pixels x pairs
+    CK(hipMalloc(&d_big, (size_t)28 * N * n));
+    CK(hipMemset(d_big, 0, (size_t)28 * N * n));
     CK(hipStreamSynchronize(c->stream));
+    printf("fast division verified: %d\n", youth_icp_fastdiv_enabled(c));
     const float thr2 = P.dist_thresh * P.dist_thresh;
-    const PairMap pm{0, n};
     hipStream_t st = c->stream;
     float* xyz = c->d_xyz;
     float4* rec = c->d_rec;
     const size_t Pp = c->P;
     const Intr Ki = c->K;
+    const FastK Fk = c->F;
     const float* T32 = c->d_T32;
-    auto R = [&](auto kern, const float* a, const float* b) {
-        return [=](dim3 g, int chunk, double* part) {
-            hipLaunchKernelGGL(kern, g, dim3(kRedThreads), 0, st, a, b, Pp, pm, T32, W, H, Ki, thr2,
-                               chunk, part, (int32_t*)nullptr);
-        };
+    const PairMap pm_v0{0, n};     // xyz frames: sources [0, n), targets [n, 2n)
+    const PairMap pm_prod{0, n};   // depth frame p of d_src, record frame n + p
+    auto V0 = [=](dim3 g, int chunk, double* part) {
+        hipLaunchKernelGGL(k_reduce_v0<false>, g, dim3(kRedThreads), 0, st, (const float*)xyz,
+                           (const float*)d_nrm, Pp, pm_v0, T32, W, H, Ki, thr2, chunk, part,
+                           (int32_t*)nullptr);
     };
-    auto R4 = [&](auto kern, const float4* r) {
+    auto PROD = [=](auto kern) {
         return [=](dim3 g, int chunk, double* part) {
-            hipLaunchKernelGGL(kern, g, dim3(kRedThreads), 0, st, (const float*)xyz, r, Pp, pm, T32,
-                               W, H, Ki, thr2, chunk, part, (int32_t*)nullptr);
-        };
-    };
-    auto R3 = [&](auto kern, const float4* r) {
-        return [=](dim3 g, int chunk, double* part) {
-            hipLaunchKernelGGL(kern, g, dim3(kRedThreads), 0, st, (const float*)xyz,
-                               (const int16_t*)d_src, r, Pp, pm, T32, W, H, Ki, thr2, chunk, part,
-                               (int32_t*)nullptr);
+            hipLaunchKernelGGL(kern, g, dim3(kRedThreads), 0, st, (const int16_t*)d_src,
+                               (const float4*)rec, Pp, pm_prod, T32, W, H, Ki, Fk, thr2, chunk,
+                               part, (int32_t*)nullptr);
         };
     };
     std::vector<Variant> all = {
-        {"v0 planes fp64 tb2048", 2048, 36, R(k_reduce_v0<false>, xyz, d_nrm)},
-        {"prod rec16 tb2048", 2048, 28, R4(k_reduce<false>, rec)},
-        {"prod rec16 tb4096", 4096, 28, R4(k_reduce<false>, rec)},
-        {"prod rec16 tb1024", 1024, 28, R4(k_reduce<false>, rec)},
-        {"r1 rec16 srcDepth tb2048", 2048, 18, R3(k_reduce3<false, 1>, rec)},
-        {"v5 pipe planes tb4096", 4096, 36, R(k_reduce2<false, double>, xyz, d_nrm)},
+        {"v0 planes fp64 tb2048", 2048, 36, V0},
+        {"prod fast aligned tb2048", 2048, 18, PROD(k_reduce<false, true, true>)},
+        {"prod fast aligned tb4096", 4096, 18, PROD(k_reduce<false, true, true>)},
+        {"prod fast aligned tb1024", 1024, 18, PROD(k_reduce<false, true, true>)},
+        {"prod ieee aligned tb2048", 2048, 18, PROD(k_reduce<false, false, true>)},
+        {"prod fast unaligned tb2048", 2048, 18, PROD(k_reduce<false, true, false>)},
+        // streaming-read calibration over 28 B/px x pixels x pairs
+        {"s0 stream dwordx4 28B/px", 2048, 28, [=](dim3, int, double* part) {
+             hipLaunchKernelGGL(k_stream_read, dim3(2048), dim3(256), 0, st, (const float4*)d_big,
+                                (size_t)28 * N * n / 16, (float*)part);
+         }},
+        {"s1 stream dword 28B/px", 2048, 28, [=](dim3, int, double* part) {
+             hipLaunchKernelGGL(k_stream_read1, dim3(2048), dim3(256), 0, st, (const float*)d_big,
+                                (size_t)28 * N * n / 4, (float*)part);
+         }},
     };
     std::vector<Variant> vs;
     for (auto& v : all)
