@@ -340,3 +340,23 @@ def test_unaligned_source_pointer():
     for p in range(2):
         To, _, sto, _ = oracle.align(src[p], dst[p])
         assert st[p] == sto and _pose_err(T64[p], To) <= POSE_TOL
+
+
+def test_plain_c_host_demo(tmp_path):
+    """The drop-in driven from plain C99 (pthread algorithmModule +
+    processSlamFrame + saveSlamMap), as the reference's main.c would."""
+    import subprocess
+    from conftest import PKG
+    exe = os.path.join(PKG, "slam_host_demo")
+    base = str(tmp_path / "demo")
+    r = subprocess.run([exe, os.path.join(GOLDEN, "astra_camera.yaml"), "6", base],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    rows = np.loadtxt(base + "_trajectory.txt")
+    assert rows.shape == (6, 8)
+    frames, _ = youth_synth.sequence(0, 6)
+    acc = np.eye(4)
+    for k in range(1, 6):
+        T64, _, _, _ = oracle.align(frames[k], frames[k - 1])
+        acc = acc @ T64
+    assert np.allclose(rows[-1, 1:4], acc[:3, 3], atol=1e-6)
