@@ -1,13 +1,19 @@
 #!/usr/bin/env python3
 """Benchmark: ICP frame-pair aligns/sec @640x480 on 1..N MI355X.
 
-A "step" = one pass of the hot path over one batch: every rank aligns its
-shard of independent 640x480 pairs (back-project both frames, target normals,
-10 fixed point-to-plane iterations, final pose on device), then the poses are
-all-gathered over RCCL (N > 1).  Inputs are synthetic depth (libyouth_synth),
-resident in HBM before the timed region.  Per-GPU work is fixed (weak
-scaling); the default shard is BASELINE config C4's per-GPU share (64 pairs),
-so N = 8 is exactly C4's 512-pair batch.
+Default workload ("pairs", BASELINE config C4 per-GPU share): a "step" is one
+pass of the hot path over one batch — every rank aligns its 64 independent
+640x480 pairs (target records, 10 fixed point-to-plane iterations, final
+pose on device), then the fp32 poses are all-gathered over RCCL (N > 1).
+Inputs are synthetic int16 depth (libyouth_synth), resident in HBM before
+the timed region.  Per-GPU work is fixed (weak scaling); N = 8 is exactly
+C4's 512-pair batch.
+
+`--workload sequence` (config C5): a streamed synthetic sequence of
+--frames frames (default 1000) split over the ranks with a 1-frame halo;
+each step aligns every (k, k+1) pair (each frame prepared once), gathers the
+relative poses and composes the trajectory on rank 0.  Total work is fixed
+(strong scaling).
 
 Launch: python bench.py [--gpus 1] [--steps K] [--warmup W]
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -28,6 +34,7 @@ sys.path.insert(0, os.path.join(ROOT, "slam-rgbd_amd"))
 
 import numpy as np  # noqa: E402
 
+import youth_dist  # noqa: E402
 import youth_icp  # noqa: E402
 import youth_synth  # noqa: E402
 
@@ -42,90 +49,168 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", choices=["pairs", "sequence"], default="pairs")
     ap.add_argument("--pairs-per-gpu", type=int, default=64)
+    ap.add_argument("--frames", type=int, default=1000, help="sequence workload length")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpus)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
-                    help="PMC-derived HBM bytes per reduction launch (from tools/pmc_traffic.py)")
+                    help="PMC-derived HBM bytes per k_reduce launch (tools/pmc_traffic.py)")
     return ap.parse_args()
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        a.gpus = world if world > 1 else a.gpus
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+class Run:
+    def __init__(self, a):
+        self.a = a
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(self.local)
+        if self.world > 1:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
 
+    def barrier_sync(self):
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def timed(self, ctx, step):
+        a = self.a
+        for _ in range(a.warmup):
+            step()
+        self.barrier_sync()
+        ctx.set_timing(True)
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        self.barrier_sync()
+        elapsed = time.perf_counter() - t0
+        kt = {k: ctx.get_timing(i) for i, k in enumerate(("k_reduce", "k_solve", "k_prep"))}
+        ctx.set_timing(False)
+        if self.world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        return elapsed, kt
+
+    def roofline(self, kt, pixels_per_launch):
+        red_ms, red_n = kt["k_reduce"]
+        avg = red_ms / max(red_n, 1)
+        alg = BYTES_PER_PX_ITER * pixels_per_launch
+        own = KERNEL_BYTES_PER_PX * pixels_per_launch
+        traffic, src = None, None
+        if os.path.exists(self.a.traffic_json):
+            try:
+                tj = json.load(open(self.a.traffic_json))
+                if tj.get("width") == self.a.width and tj.get("height") == self.a.height and \
+                        tj.get("pairs") * self.a.width * self.a.height == pixels_per_launch:
+                    traffic, src = tj.get("hbm_bytes_per_launch"), \
+                        os.path.relpath(self.a.traffic_json, ROOT)
+            except (OSError, ValueError, TypeError):
+                traffic = None
+        achieved = alg / (avg * 1e-3) / 1e9
+        return {
+            "bound": "hbm", "kernel": "k_reduce",
+            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
+            "algorithmic_bytes_per_launch": alg,
+            "algorithmic_model": "SURVEY §8d: 36 B/px/iter x pixels x pairs",
+            "kernel_bytes_per_launch": own,
+            "achieved_kernel_bytes": own / (avg * 1e-3) / 1e9,
+            "frac_kernel_bytes": own / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "avg_launch_ms": avg, "launches": red_n,
+        }
+
+    def finish(self):
+        if self.world > 1:
+            dist.destroy_process_group()
+
+
+def run_pairs(R):
+    a, world, rank = R.a, R.world, R.rank
     W, H, n = a.width, a.height, a.pairs_per_gpu
-    N = W * H
-    # rank r aligns global pairs [r*n, (r+1)*n): seeds 0x5EED0000 + global index
-    src, dst, _ = youth_synth.pairs(rank * n, n, W, H)
+    first, cnt = youth_dist.pair_shard(rank, n)      # seeds 0x5EED0000 + global index
+    src, dst, _ = youth_synth.pairs(first, cnt, W, H)
     d_src = torch.from_numpy(src).cuda()
     d_dst = torch.from_numpy(dst).cuda()
     poses = torch.zeros((n, 16), dtype=torch.float32, device="cuda")
-    gathered = torch.zeros((world * n, 16), dtype=torch.float32, device="cuda")
-    ctx = youth_icp.IcpContext(W, H, 2 * n, iters=a.iters, device=local)
+    ctx = youth_icp.IcpContext(W, H, n, iters=a.iters, device=R.local)
     stream = torch.cuda.current_stream().cuda_stream
 
     def step():
         ctx.align_pairs_device(d_src.data_ptr(), d_dst.data_ptr(), n,
                                d_T_out=poses.data_ptr(), stream=stream)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, poses)
+        youth_dist.gather_poses(poses, world)
 
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ctx.set_timing(True)
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    red_ms, red_n = ctx.get_timing(0)
-    solve_ms, solve_n = ctx.get_timing(1)
-    prep_ms, prep_n = ctx.get_timing(2)
-    ctx.set_timing(False)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, kt = R.timed(ctx, step)
+    T_gpu, _, _ = ctx.get_poses(n)          # fp64 poses of the last step
+    result = base_result(R, world * n * a.steps / elapsed, elapsed)
+    result["scaling"] = "weak"
+    result["config"] = {
+        "workload": f"C4 per-GPU shard: {n} independent {W}x{H} pairs/GPU, "
+                    f"{a.iters} point-to-plane iters (N=8 -> 512 pairs = C4)",
+        "pairs_per_gpu": n, "global_pairs": world * n, "width": W, "height": H,
+        "iters": a.iters, "fastdiv": ctx.fastdiv,
+        "parallelism": f"dp{world} (pair shards, RCCL pose all-gather)",
+    }
+    result["roofline"] = R.roofline(kt, n * W * H)
+    result["kernel_ms_per_step"] = {k: v[0] / a.steps for k, v in kt.items()}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        result["cpu_baseline"], result["parity"] = cpu_baseline(a, src, dst, T_gpu)
+    ctx.close()
+    return result
 
-    # HBM roofline of the dominant kernel (k_reduce): algorithmic bytes per launch
-    red_avg_ms = red_ms / max(red_n, 1)
-    bytes_per_launch = BYTES_PER_PX_ITER * N * n
-    achieved = bytes_per_launch / (red_avg_ms * 1e-3) / 1e9
-    traffic = None
-    traffic_src = None
-    if os.path.exists(a.traffic_json):
-        try:
-            tj = json.load(open(a.traffic_json))
-            if tj.get("pairs") == n and tj.get("width") == W and tj.get("height") == H:
-                traffic = tj.get("hbm_bytes_per_launch")
-                traffic_src = os.path.relpath(a.traffic_json, ROOT)
-        except (OSError, ValueError):
-            traffic = None
 
-    T_gpu, _, _ = ctx.get_poses(n)          # fp64 device poses of the last step
-    result = {
+def run_sequence(R):
+    a, world, rank = R.a, R.world, R.rank
+    W, H, F = a.width, a.height, a.frames
+    f0, f1 = youth_dist.sequence_shard(F, world, rank)
+    nf = f1 - f0
+    npairs = max(nf - 1, 0)
+    frames, _ = youth_synth.sequence(f0, max(nf, 2), W, H)
+    d_frames = torch.from_numpy(frames).cuda()
+    rel = torch.zeros((max(npairs, 1), 16), dtype=torch.float32, device="cuda")
+    ctx = youth_icp.IcpContext(W, H, max(npairs, 2), iters=a.iters, device=R.local)
+    stream = torch.cuda.current_stream().cuda_stream
+    max_rows = (F - 1 + world - 1) // world
+    traj = {}
+
+    def step():
+        if npairs:
+            ctx.align_sequence_device(d_frames.data_ptr(), nf, d_T_out=rel.data_ptr(),
+                                      stream=stream)
+        rows = youth_dist.gather_ragged(rel[:npairs], world, max_rows)
+        if rank == 0:
+            traj["T"] = rows   # composed after the timed region (host, ordered fp64)
+
+    elapsed, kt = R.timed(ctx, step)
+    result = base_result(R, (F - 1) * a.steps / elapsed, elapsed)
+    result["scaling"] = "strong"
+    result["config"] = {
+        "workload": f"C5: {F}-frame synthetic sequence, {W}x{H}, streamed frame-to-frame "
+                    f"odometry, {a.iters} iters, {F - 1} pairs split over ranks (1-frame halo)",
+        "frames": F, "pairs": F - 1, "width": W, "height": H, "iters": a.iters,
+        "parallelism": f"dp{world} (contiguous pair ranges, RCCL pose gather)",
+    }
+    result["roofline"] = R.roofline(kt, max(npairs, 1) * W * H)
+    if rank == 0:
+        T = youth_dist.compose_trajectory(traj["T"].cpu().numpy().reshape(-1, 4, 4))
+        result["trajectory_frames"] = int(T.shape[0])
+    ctx.close()
+    return result
+
+
+def base_result(R, value, elapsed):
+    a = R.a
+    return {
         "metric": METRIC,
-        "value": world * n * a.steps / elapsed,
+        "value": value,
         "unit": "aligns/s",
-        "n_gpus": world,
+        "n_gpus": R.world,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": elapsed / a.steps * 1e3,
@@ -133,39 +218,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic (ray-cast room scene, int16 mm depth, seeds 0x5EED0000+pair)",
-        "config": {
-            "workload": f"C4 per-GPU shard: {n} independent {W}x{H} pairs/GPU, "
-                        f"{a.iters} point-to-plane iters (N=8 -> 512 pairs = C4)",
-            "pairs_per_gpu": n, "global_pairs": world * n, "width": W, "height": H,
-            "iters": a.iters,
-            "parallelism": f"dp{world} (pair shards, RCCL pose all-gather)",
-        },
-        "roofline": {
-            "bound": "hbm", "kernel": "k_reduce",
-            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "traffic_source": traffic_src,
-            "algorithmic_bytes_per_launch": bytes_per_launch,
-            "algorithmic_model": "SURVEY §8d: 36 B/px/iter x pixels x pairs",
-            "kernel_bytes_per_launch": KERNEL_BYTES_PER_PX * N * n,
-            "achieved_kernel_bytes": KERNEL_BYTES_PER_PX * N * n / (red_avg_ms * 1e-3) / 1e9,
-            "frac_kernel_bytes": KERNEL_BYTES_PER_PX * N * n / (red_avg_ms * 1e-3) / 1e9
-            / HBM_PEAK_GBS,
-            "avg_launch_ms": red_avg_ms, "launches": red_n,
-        },
-        "kernel_ms_per_step": {
-            "k_reduce": red_ms / a.steps, "k_solve": solve_ms / a.steps,
-            "k_prep": prep_ms / a.steps,
-        },
+        "data": "synthetic (ray-cast room scene, int16 mm depth, seeds 0x5EED0000+pair / "
+                "0x5EED1000 sequence)",
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        result["cpu_baseline"], result["parity"] = cpu_baseline(a, src, dst, T_gpu)
-    if rank == 0:
-        print(json.dumps(result), flush=True)
-    ctx.close()
-    if world > 1:
-        dist.destroy_process_group()
 
 
 def cpu_baseline(a, src, dst, T_gpu):
@@ -176,7 +231,7 @@ def cpu_baseline(a, src, dst, T_gpu):
 
     cpus = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     threads = a.cpu_threads or min(16, cpus or 1)
-    S = a.pairs_per_gpu
+    S = src.shape[0]
     oracle.align_batch(src[:1], dst[:1], iters=a.iters, n_threads=1)  # warm
     # repeat passes over the rank-0 pairs until ~1.5 s wall (~10-30 s of CPU work)
     passes, wall, T_cpu, st = 0, 0.0, None, None
@@ -193,6 +248,15 @@ def cpu_baseline(a, src, dst, T_gpu):
     parity = {"pose_max_abs_err_vs_cpu": err, "pairs_checked": S, "tolerance": 1e-5,
               "cpu_status_nonzero": int((st != 0).sum())}
     return cpu, parity
+
+
+def main():
+    a = parse()
+    R = Run(a)
+    result = run_pairs(R) if a.workload == "pairs" else run_sequence(R)
+    if R.rank == 0:
+        print(json.dumps(result), flush=True)
+    R.finish()
 
 
 if __name__ == "__main__":

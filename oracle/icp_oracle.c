@@ -175,18 +175,19 @@ int oracle_solve(const double neq[ORACLE_NEQ], double xi[6])
         if (A[a][a] > maxd) maxd = A[a][a];
     if (!(maxd > 0.0)) return 1;
     const double eps = 1e-12 * maxd;
-    double L[6][6], D[6];
+    double L[6][6], D[6], Dinv[6];
     memset(L, 0, sizeof(L));
     for (int j = 0; j < 6; ++j) {
         double d = A[j][j];
         for (int m = 0; m < j; ++m) d -= (L[j][m] * L[j][m]) * D[m];
         if (!(d > eps)) return 1;
         D[j] = d;
+        Dinv[j] = 1.0 / d;  /* one divide per pivot; every use multiplies */
         L[j][j] = 1.0;
         for (int i = j + 1; i < 6; ++i) {
             double s = A[i][j];
             for (int m = 0; m < j; ++m) s -= (L[i][m] * L[j][m]) * D[m];
-            L[i][j] = s / d;
+            L[i][j] = s * Dinv[j];
         }
     }
     double y[6], x[6];
@@ -195,7 +196,7 @@ int oracle_solve(const double neq[ORACLE_NEQ], double xi[6])
         for (int m = 0; m < i; ++m) s -= L[i][m] * y[m];
         y[i] = s;
     }
-    for (int i = 0; i < 6; ++i) y[i] = y[i] / D[i];
+    for (int i = 0; i < 6; ++i) y[i] = y[i] * Dinv[i];
     for (int i = 5; i >= 0; --i) {
         double s = y[i];
         for (int m = i + 1; m < 6; ++m) s -= L[m][i] * x[m];

@@ -124,7 +124,7 @@ __global__ void k_verify_fastdiv(Intr K, FastK F, int W, int H, unsigned* bad)
 // n = normalize((P(u+1)-P(u-1)) x (P(v+1)-P(v-1))); (0,0,0) on the 1-px
 // border, if the centre or any of the 4 neighbours is invalid, or if the
 // cross product is zero; oriented so n.P <= 0.
-template <bool kFast>
+template <bool kFast, bool kWide>
 __global__ __launch_bounds__(kPrepThreads) void k_prep(const int16_t* __restrict__ depth, int out0,
                                                       int W, int H, size_t P, Intr K, FastK F,
                                                       float4* __restrict__ recs,
@@ -143,16 +143,43 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const int16_t* __restrict
     const int tx = threadIdx.x & 63;
     const int ty = threadIdx.x >> 6;
 
-    for (int e = threadIdx.x; e < kLdsH * kLdsW; e += kPrepThreads) {
-        const int ly = e / kLdsW;
-        const int lx = e - ly * kLdsW;
-        const int gx = x0 - 1 + lx, gy = y0 - 1 + ly;
-        float x = 0.0f, y = 0.0f, z = 0.0f;
-        if (gx >= 0 && gx < W && gy >= 0 && gy < H)
-            backproject<kFast>(dep[(size_t)gy * W + gx], gx, gy, K, F, x, y, z);
-        sX[ly][lx] = x;
-        sY[ly][lx] = y;
-        sZ[ly][lx] = z;
+    if (kWide) {
+        // W % 4 == 0 (and an 8-byte-aligned frame): columns [x0-4, x0+68) as
+        // 18 aligned 8-byte words per halo row; each word's 4 pixels are all
+        // inside or all outside the image, so no lane straddles an edge.
+        constexpr int kWords = (kTileW + 8) / 4;  // 18
+        for (int e = threadIdx.x; e < kLdsH * kWords; e += kPrepThreads) {
+            const int ly = e / kWords;
+            const int m = e - ly * kWords;
+            const int gy = y0 - 1 + ly;
+            const int c = x0 - 4 + 4 * m;
+            short4 d4 = make_short4(0, 0, 0, 0);
+            if (gy >= 0 && gy < H && c >= 0 && c < W)
+                d4 = *reinterpret_cast<const short4*>(dep + (size_t)gy * W + c);
+            const int dv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int lx = 4 * m - 3 + q;  // LDS column of pixel c + q
+                if (lx < 0 || lx >= kLdsW) continue;
+                float x, y, z;
+                backproject<kFast>(dv[q], c + q, gy, K, F, x, y, z);
+                sX[ly][lx] = x;
+                sY[ly][lx] = y;
+                sZ[ly][lx] = z;
+            }
+        }
+    } else {
+        for (int e = threadIdx.x; e < kLdsH * kLdsW; e += kPrepThreads) {
+            const int ly = e / kLdsW;
+            const int lx = e - ly * kLdsW;
+            const int gx = x0 - 1 + lx, gy = y0 - 1 + ly;
+            float x = 0.0f, y = 0.0f, z = 0.0f;
+            if (gx >= 0 && gx < W && gy >= 0 && gy < H)
+                backproject<kFast>(dep[(size_t)gy * W + gx], gx, gy, K, F, x, y, z);
+            sX[ly][lx] = x;
+            sY[ly][lx] = y;
+            sZ[ly][lx] = z;
+        }
     }
     __syncthreads();
 
@@ -203,155 +230,6 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const int16_t* __restrict
     }
 }
 
-// ---------------------------------------------------------------- k_reduce --
-// Spec a7-a9 for four consecutive source pixels per lane per step.
-//   source  int16 depth (2 B/px), back-projected in registers (8-byte load
-//           per lane when the frame is 8-byte aligned and N % 4 == 0);
-//   target  ONE aligned 16-byte record fetch {z, nx, ny, nz} per pixel; the
-//           target's x, y are recomputed from z with k_prep's expression, so
-//           they are bit-identical to what k_prep would have stored.
-// Branch-free: invalid lanes compute on safe values and are masked, so the
-// four fetches issue back to back.  Accumulators are fp64 fed with exact
-// fp32 products: the result equals the oracle's row-major fp64 sum up to
-// fp64 summation order.  (tools/kbench: 205 us for the first SoA version ->
-// 107 us for this one at 64 pairs, partial sums unchanged.)
-struct PairMap {
-    int src0, tgt0;  // pair p: source depth frame src0 + p, target record frame tgt0 + p
-};
-
-template <bool kAligned>
-__device__ __forceinline__ short4 load_depth4(const int16_t* __restrict__ sD, int i, int end)
-{
-    // i < end always here; kAligned => i % 4 == 0 and i + 3 < end
-    short4 d;
-    if (kAligned) {
-        d = *reinterpret_cast<const short4*>(sD + i);
-    } else {
-        d.x = sD[i];
-        d.y = (i + 1) < end ? sD[i + 1] : (short)0;
-        d.z = (i + 2) < end ? sD[i + 2] : (short)0;
-        d.w = (i + 3) < end ? sD[i + 3] : (short)0;
-    }
-    return d;
-}
-
-template <bool kAssoc, bool kFast, bool kAligned>
-__global__ __launch_bounds__(kRedThreads) void k_reduce(
-    const int16_t* __restrict__ dsrc, const float4* __restrict__ recs, size_t P, PairMap pm,
-    const float* __restrict__ T32, int W, int H, Intr K, FastK F, float thr2, int chunk,
-    double* __restrict__ partials, int32_t* __restrict__ assoc)
-{
-    __shared__ double red[kRedThreads / 64][kNeq];
-    const int p = blockIdx.y;
-    const int b = blockIdx.x;
-    const int N = W * H;
-    const int16_t* sD = dsrc + (size_t)(pm.src0 + p) * N;
-    const float4* rec = recs + (size_t)(pm.tgt0 + p) * P;
-    float T[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) T[k] = T32[p * 12 + k];
-
-    double acc[kNeq];
-#pragma unroll
-    for (int k = 0; k < kNeq; ++k) acc[k] = 0.0;
-
-    const int start = b * chunk;
-    const int end = min(start + chunk, N);
-    int32_t* arow = kAssoc ? assoc + (size_t)p * N : nullptr;
-    for (int i = start + threadIdx.x * 4; i < end; i += kRedStep) {
-        const short4 d4 = load_depth4<kAligned>(sD, i, end);
-        const int dd[4] = {d4.x, d4.y, d4.z, d4.w};
-        const int v0 = i / W;
-        const int u0 = i - v0 * W;
-        // spec a7: P' = R P + t (fixed order, no FMA); projective association
-        float qx[4], qy[4], qz[4], fu[4], fv[4];
-        int j[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            int u = u0 + q, v = v0;
-            if (u >= W) {
-                u -= W;
-                ++v;
-            }
-            float sx, sy, sz;
-            backproject<kFast>((i + q) < end ? dd[q] : 0, u, v, K, F, sx, sy, sz);
-            qx[q] = ((T[0] * sx + T[1] * sy) + T[2] * sz) + T[3];
-            qy[q] = ((T[4] * sx + T[5] * sy) + T[6] * sz) + T[7];
-            qz[q] = ((T[8] * sx + T[9] * sy) + T[10] * sz) + T[11];
-            const bool vz = sz > 0.0f && qz[q] > 0.0f;
-            const float qzs = vz ? qz[q] : 1.0f;
-            const float uu = floorf((((K.fx * qx[q]) / qzs) + K.cx) + 0.5f);
-            const float vv = floorf((((K.fy * qy[q]) / qzs) + K.cy) + 0.5f);
-            const bool in = vz && uu >= 0.0f && uu < (float)W && vv >= 0.0f && vv < (float)H;
-            fu[q] = in ? uu : 0.0f;
-            fv[q] = in ? vv : 0.0f;
-            j[q] = in ? (int)fv[q] * W + (int)fu[q] : -1;
-        }
-        // four 16-byte fetches back to back (clamped index: no branch)
-        float4 t[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) t[q] = rec[j[q] >= 0 ? j[q] : 0];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const float tz = t[q].x;
-            const float tx = bp_div<kFast>((fu[q] - K.cx) * tz, K.fx, F.rfx);
-            const float ty = bp_div<kFast>((fv[q] - K.cy) * tz, K.fy, F.rfy);
-            const float nx = t[q].y, ny = t[q].z, nz = t[q].w;
-            const float dx = qx[q] - tx, dy = qy[q] - ty, dz = qz[q] - tz;
-            const float d2 = (dx * dx + dy * dy) + dz * dz;
-            const bool nvalid = !(nx == 0.0f && ny == 0.0f && nz == 0.0f);
-            const bool ok = j[q] >= 0 && tz > 0.0f && nvalid && d2 < thr2;
-            if (kAssoc && (i + q) < end) arow[i + q] = ok ? j[q] : -1;
-            // spec a8: r = n.(P' - P_t); J = [P' x n, n]  (zeros when unmatched)
-            const float n0 = ok ? nx : 0.0f, n1 = ok ? ny : 0.0f, n2 = ok ? nz : 0.0f;
-            const float r = ok ? (nx * dx + ny * dy) + nz * dz : 0.0f;
-            float Jf[6];
-            Jf[0] = qy[q] * n2 - qz[q] * n1;
-            Jf[1] = qz[q] * n0 - qx[q] * n2;
-            Jf[2] = qx[q] * n1 - qy[q] * n0;
-            Jf[3] = n0;
-            Jf[4] = n1;
-            Jf[5] = n2;
-            // spec a9: fp32 products are exact in fp64; one rounding per add
-            int k = 0;
-#pragma unroll
-            for (int a = 0; a < 6; ++a)
-#pragma unroll
-                for (int bb = a; bb < 6; ++bb) {
-                    acc[k] = fma((double)Jf[a], (double)Jf[bb], acc[k]);
-                    ++k;
-                }
-#pragma unroll
-            for (int a = 0; a < 6; ++a) acc[21 + a] = fma((double)Jf[a], (double)r, acc[21 + a]);
-            acc[27] = fma((double)r, (double)r, acc[27]);
-            acc[28] += ok ? 1.0 : 0.0;
-        }
-    }
-
-    // wave butterfly (lane-symmetric: every lane ends with the same sum),
-    // then the four waves in fixed order through LDS
-#pragma unroll
-    for (int k = 0; k < kNeq; ++k) {
-        double v = acc[k];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-        acc[k] = v;
-    }
-    const int wave = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-        for (int k = 0; k < kNeq; ++k) red[wave][k] = acc[k];
-    }
-    __syncthreads();
-    if (threadIdx.x < kNeq) {
-        const int k = threadIdx.x;
-        double s = red[0][k];
-#pragma unroll
-        for (int w = 1; w < kRedThreads / 64; ++w) s += red[w][k];
-        partials[((size_t)p * gridDim.x + b) * kNeq + k] = s;
-    }
-}
-
 // ----------------------------------------------------------------- k_solve --
 // LDL^T + SE(3) exp, same algorithm and evaluation order as oracle_solve /
 // oracle_se3_exp (oracle/icp_oracle.c).
@@ -372,7 +250,7 @@ __device__ int solve6(const double* neq, double xi[6])
         if (A[a][a] > maxd) maxd = A[a][a];
     if (!(maxd > 0.0)) return YOUTH_STATUS_DEGENERATE;
     const double eps = 1e-12 * maxd;
-    double L[6][6], D[6];
+    double L[6][6], D[6], Dinv[6];
     for (int i = 0; i < 6; ++i)
         for (int j = 0; j < 6; ++j) L[i][j] = 0.0;
     for (int j = 0; j < 6; ++j) {
@@ -380,11 +258,12 @@ __device__ int solve6(const double* neq, double xi[6])
         for (int m = 0; m < j; ++m) d -= (L[j][m] * L[j][m]) * D[m];
         if (!(d > eps)) return YOUTH_STATUS_DEGENERATE;
         D[j] = d;
+        Dinv[j] = 1.0 / d;  /* one divide per pivot; every use multiplies */
         L[j][j] = 1.0;
         for (int i = j + 1; i < 6; ++i) {
             double s = A[i][j];
             for (int m = 0; m < j; ++m) s -= (L[i][m] * L[j][m]) * D[m];
-            L[i][j] = s / d;
+            L[i][j] = s * Dinv[j];
         }
     }
     double y[6], x[6];
@@ -393,7 +272,7 @@ __device__ int solve6(const double* neq, double xi[6])
         for (int m = 0; m < i; ++m) s -= L[i][m] * y[m];
         y[i] = s;
     }
-    for (int i = 0; i < 6; ++i) y[i] = y[i] / D[i];
+    for (int i = 0; i < 6; ++i) y[i] = y[i] * Dinv[i];
     for (int i = 5; i >= 0; --i) {
         double s = y[i];
         for (int m = i + 1; m < 6; ++m) s -= L[m][i] * x[m];
@@ -539,6 +418,225 @@ __global__ void k_export(const double* __restrict__ T64, int n, float* __restric
     out[t] = i < 12 ? (float)T64[(size_t)(t >> 4) * 16 + i] : (i == 15 ? 1.0f : 0.0f);
 }
 
+// ---------------------------------------------------------------- k_reduce --
+// Spec a7-a9 for four consecutive source pixels per lane per step.
+//   source  int16 depth (2 B/px), back-projected in registers (8-byte load
+//           per lane when the frame is 8-byte aligned and N % 4 == 0);
+//   target  ONE aligned 16-byte record fetch {z, nx, ny, nz} per pixel; the
+//           target's x, y are recomputed from z with k_prep's expression, so
+//           they are bit-identical to what k_prep would have stored.
+// Branch-free: invalid lanes compute on safe values and are masked, so the
+// four fetches issue back to back.  Accumulators are fp64 fed with exact
+// fp32 products: the result equals the oracle's row-major fp64 sum up to
+// fp64 summation order.  (tools/kbench: 205 us for the first SoA version ->
+// 107 us for this one at 64 pairs, partial sums unchanged.)
+struct PairMap {
+    int src0, tgt0;  // pair p: source depth frame src0 + p, target record frame tgt0 + p
+};
+
+template <bool kAligned>
+__device__ __forceinline__ short4 load_depth4(const int16_t* __restrict__ sD, int i, int end)
+{
+    // i < end always here; kAligned => i % 4 == 0 and i + 3 < end
+    short4 d;
+    if (kAligned) {
+        d = *reinterpret_cast<const short4*>(sD + i);
+    } else {
+        d.x = sD[i];
+        d.y = (i + 1) < end ? sD[i + 1] : (short)0;
+        d.z = (i + 2) < end ? sD[i + 2] : (short)0;
+        d.w = (i + 3) < end ? sD[i + 3] : (short)0;
+    }
+    return d;
+}
+
+// Per-iteration pose state for the fused solve (kFuse).  T32 is read by
+// every workgroup of pair p at entry and rewritten only by p's LAST
+// workgroup, after all of p's workgroups have arrived (so after they read it).
+struct PoseState {
+    double* T64;          // [pair][16]
+    float* T32;           // [pair][12]
+    int32_t* status;      // [pair]
+    double* stats;        // [pair][iters][2] or null
+    unsigned* arrivals;   // [pair], zero at launch; re-armed by the last arriver
+    int it, iters;
+};
+
+template <bool kAssoc, bool kFast, bool kAligned, bool kFuse>
+__global__ __launch_bounds__(kRedThreads) void k_reduce(
+    const int16_t* __restrict__ dsrc, const float4* __restrict__ recs, size_t P, PairMap pm,
+    int W, int H, Intr K, FastK F, float thr2, int chunk, double* __restrict__ partials,
+    int32_t* __restrict__ assoc, PoseState ps)
+{
+    __shared__ double red[kRedThreads / 64][kNeq];
+    const int p = blockIdx.y;
+    const int b = blockIdx.x;
+    const int N = W * H;
+    const int16_t* sD = dsrc + (size_t)(pm.src0 + p) * N;
+    const float4* rec = recs + (size_t)(pm.tgt0 + p) * P;
+    float T[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) T[k] = ps.T32[p * 12 + k];
+
+    double acc[kNeq];
+#pragma unroll
+    for (int k = 0; k < kNeq; ++k) acc[k] = 0.0;
+
+    const int start = b * chunk;
+    const int end = min(start + chunk, N);
+    int32_t* arow = kAssoc ? assoc + (size_t)p * N : nullptr;
+    for (int i = start + threadIdx.x * 4; i < end; i += kRedStep) {
+        const short4 d4 = load_depth4<kAligned>(sD, i, end);
+        const int dd[4] = {d4.x, d4.y, d4.z, d4.w};
+        const int v0 = i / W;
+        const int u0 = i - v0 * W;
+        // spec a7: P' = R P + t (fixed order, no FMA); projective association
+        float qx[4], qy[4], qz[4], fu[4], fv[4];
+        int j[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            int u = u0 + q, v = v0;
+            if (u >= W) {
+                u -= W;
+                ++v;
+            }
+            float sx, sy, sz;
+            backproject<kFast>((i + q) < end ? dd[q] : 0, u, v, K, F, sx, sy, sz);
+            qx[q] = ((T[0] * sx + T[1] * sy) + T[2] * sz) + T[3];
+            qy[q] = ((T[4] * sx + T[5] * sy) + T[6] * sz) + T[7];
+            qz[q] = ((T[8] * sx + T[9] * sy) + T[10] * sz) + T[11];
+            const bool vz = sz > 0.0f && qz[q] > 0.0f;
+            const float qzs = vz ? qz[q] : 1.0f;
+            const float uu = floorf((((K.fx * qx[q]) / qzs) + K.cx) + 0.5f);
+            const float vv = floorf((((K.fy * qy[q]) / qzs) + K.cy) + 0.5f);
+            const bool in = vz && uu >= 0.0f && uu < (float)W && vv >= 0.0f && vv < (float)H;
+            fu[q] = in ? uu : 0.0f;
+            fv[q] = in ? vv : 0.0f;
+            j[q] = in ? (int)fv[q] * W + (int)fu[q] : -1;
+        }
+        // four 16-byte fetches back to back (clamped index: no branch)
+        float4 t[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) t[q] = rec[j[q] >= 0 ? j[q] : 0];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float tz = t[q].x;
+            const float tx = bp_div<kFast>((fu[q] - K.cx) * tz, K.fx, F.rfx);
+            const float ty = bp_div<kFast>((fv[q] - K.cy) * tz, K.fy, F.rfy);
+            const float nx = t[q].y, ny = t[q].z, nz = t[q].w;
+            const float dx = qx[q] - tx, dy = qy[q] - ty, dz = qz[q] - tz;
+            const float d2 = (dx * dx + dy * dy) + dz * dz;
+            const bool nvalid = !(nx == 0.0f && ny == 0.0f && nz == 0.0f);
+            const bool ok = j[q] >= 0 && tz > 0.0f && nvalid && d2 < thr2;
+            if (kAssoc && (i + q) < end) arow[i + q] = ok ? j[q] : -1;
+            // spec a8: r = n.(P' - P_t); J = [P' x n, n]  (zeros when unmatched)
+            const float n0 = ok ? nx : 0.0f, n1 = ok ? ny : 0.0f, n2 = ok ? nz : 0.0f;
+            const float r = ok ? (nx * dx + ny * dy) + nz * dz : 0.0f;
+            float Jf[6];
+            Jf[0] = qy[q] * n2 - qz[q] * n1;
+            Jf[1] = qz[q] * n0 - qx[q] * n2;
+            Jf[2] = qx[q] * n1 - qy[q] * n0;
+            Jf[3] = n0;
+            Jf[4] = n1;
+            Jf[5] = n2;
+            // spec a9: fp32 products are exact in fp64; one rounding per add
+            int k = 0;
+#pragma unroll
+            for (int a = 0; a < 6; ++a)
+#pragma unroll
+                for (int bb = a; bb < 6; ++bb) {
+                    acc[k] = fma((double)Jf[a], (double)Jf[bb], acc[k]);
+                    ++k;
+                }
+#pragma unroll
+            for (int a = 0; a < 6; ++a) acc[21 + a] = fma((double)Jf[a], (double)r, acc[21 + a]);
+            acc[27] = fma((double)r, (double)r, acc[27]);
+            acc[28] += ok ? 1.0 : 0.0;
+        }
+    }
+
+    // wave butterfly (lane-symmetric: every lane ends with the same sum),
+    // then the four waves in fixed order through LDS
+#pragma unroll
+    for (int k = 0; k < kNeq; ++k) {
+        double v = acc[k];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        acc[k] = v;
+    }
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int k = 0; k < kNeq; ++k) red[wave][k] = acc[k];
+    }
+    __syncthreads();
+    if (threadIdx.x >= 64) return;  // wave 0 publishes (and, if last, solves)
+    const int lane = threadIdx.x;
+    const int nblk = gridDim.x;
+    double* mine = partials + ((size_t)p * nblk + b) * kNeq;
+    double s = 0.0;
+    if (lane < kNeq) {
+#pragma unroll
+        for (int w = 0; w < kRedThreads / 64; ++w) s += red[w][lane];
+    }
+    if (!kFuse) {
+        if (lane < kNeq) mine[lane] = s;
+        return;
+    }
+    // In-launch hand-off (cdna_hip_programming.md G16, MI355X_MICROARCH.md
+    // "Valid forms" row 1): write-through (sc1) partial stores, the storing
+    // wave drains them, then ONE agent-scope atomic per workgroup; the
+    // workgroup whose add returns nblk-1 is last and reads every partial of
+    // pair p with sc1 loads only.
+    if (lane < kNeq)
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(mine) + lane,
+                           (unsigned long long)__double_as_longlong(s), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned ticket = 0;
+    if (lane == 0)
+        ticket = __hip_atomic_fetch_add(ps.arrivals + p, 1u, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+    ticket = __shfl(ticket, 0, 64);
+    if (ticket != (unsigned)nblk - 1) return;
+    // No acquire fence: every load of the handed-off partials below is an
+    // sc1 load and every store of them was an sc1 store drained before the
+    // add (G16: the fence may then be dropped).  Fixed-order sum of pair p's
+    // partials (same order as k_solve), loads issued in batches of 8.
+    const unsigned long long* base =
+        reinterpret_cast<const unsigned long long*>(partials + (size_t)p * nblk * kNeq);
+    const int half = (nblk + 1) >> 1;
+    const int k = lane & 31;
+    double t = 0.0;
+    if (k < kNeq) {
+        const int b0 = lane < 32 ? 0 : half;
+        const int b1 = lane < 32 ? half : nblk;
+        for (int bb = b0; bb < b1; bb += 8) {
+            double v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                v[q] = bb + q < b1 ? __longlong_as_double((long long)__hip_atomic_load(
+                                         base + (size_t)(bb + q) * kNeq + k, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT))
+                                   : 0.0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) t += v[q];
+        }
+    }
+    t += __shfl_down(t, 32, 64);
+    double neq[kNeq];
+#pragma unroll
+    for (int q = 0; q < kNeq; ++q) neq[q] = __shfl(t, q, 64);
+    if (lane == 0) {
+        ps.arrivals[p] = 0;  // re-armed for the next launch (stream order)
+        if (ps.stats) {
+            ps.stats[((size_t)p * ps.iters + ps.it) * 2 + 0] = neq[28];
+            ps.stats[((size_t)p * ps.iters + ps.it) * 2 + 1] = neq[27];
+        }
+        solve_update(neq, ps.T64 + (size_t)p * 16, ps.T32 + (size_t)p * 12, ps.status + p);
+    }
+}
+
 }  // namespace
 
 // =============================================================== host side ==
@@ -594,6 +692,7 @@ struct youth_icp_ctx {
     int32_t* d_assoc = nullptr;
     float* d_Tout = nullptr;  // [max_frames][16]
     unsigned* d_flag = nullptr;
+    unsigned* d_arrivals = nullptr;  // [max_frames] fused-solve arrival counters
 
     int last_pairs = 0;
     int last_iters = 0;
@@ -714,27 +813,28 @@ static int launch_prep(youth_icp_ctx* c, hipStream_t s, const int16_t* depth, in
     int rc = ev_begin(c, s, &ep, 2);
     if (rc) return rc;
     float* xyz = want_xyz ? c->d_xyz : nullptr;
-    if (c->fast)
-        hipLaunchKernelGGL(k_prep<true>, grid, dim3(kPrepThreads), 0, s, depth, out0, c->W, c->H,
-                           c->P, c->K, c->F, c->d_rec, xyz);
-    else
-        hipLaunchKernelGGL(k_prep<false>, grid, dim3(kPrepThreads), 0, s, depth, out0, c->W, c->H,
-                           c->P, c->K, c->F, c->d_rec, xyz);
+    const bool wide = (c->W % 4 == 0) && (reinterpret_cast<uintptr_t>(depth) % 8 == 0);
+    auto kern = c->fast ? (wide ? k_prep<true, true> : k_prep<true, false>)
+                        : (wide ? k_prep<false, true> : k_prep<false, false>);
+    hipLaunchKernelGGL(kern, grid, dim3(kPrepThreads), 0, s, depth, out0, c->W, c->H, c->P, c->K,
+                       c->F, c->d_rec, xyz);
     HIP_TRY(hipGetLastError());
     return ev_end(c, s, &ep);
 }
 
-template <bool kAssoc, bool kFast, bool kAligned>
+template <bool kAssoc, bool kFast, bool kAligned, bool kFuse>
 static void launch_reduce_t(youth_icp_ctx* c, hipStream_t s, dim3 grid, const int16_t* dsrc,
-                            PairMap pm, float thr2, int chunk)
+                            PairMap pm, float thr2, int chunk, const PoseState& ps)
 {
-    hipLaunchKernelGGL((k_reduce<kAssoc, kFast, kAligned>), grid, dim3(kRedThreads), 0, s, dsrc,
-                       c->d_rec, c->P, pm, c->d_T32, c->W, c->H, c->K, c->F, thr2, chunk,
-                       c->d_partials, kAssoc ? c->d_assoc : (int32_t*)nullptr);
+    hipLaunchKernelGGL((k_reduce<kAssoc, kFast, kAligned, kFuse>), grid, dim3(kRedThreads), 0, s,
+                       dsrc, c->d_rec, c->P, pm, c->W, c->H, c->K, c->F, thr2, chunk,
+                       c->d_partials, kAssoc ? c->d_assoc : (int32_t*)nullptr, ps);
 }
 
+// fuse_it >= 0: fused solve of iteration fuse_it (k_reduce's last workgroup
+// per pair updates the pose); fuse_it < 0: partials only (k_solve follows).
 static int launch_reduce(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, PairMap pm,
-                         int n_pairs, bool assoc, int* nblk_out)
+                         int n_pairs, bool assoc, int* nblk_out, int fuse_it = -1)
 {
     int chunk = 0;
     const int nb = reduce_geometry(c, n_pairs, &chunk);
@@ -750,16 +850,24 @@ static int launch_reduce(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, P
     EventPair ep{};
     rc = ev_begin(c, s, &ep, 0);
     if (rc) return rc;
-    const int sel = (assoc ? 4 : 0) | (c->fast ? 2 : 0) | (aligned ? 1 : 0);
+    const PoseState ps{c->d_T64, c->d_T32, c->d_status, c->d_stats, c->d_arrivals,
+                       fuse_it < 0 ? 0 : fuse_it, c->prm.iters};
+    const bool fuse = fuse_it >= 0;
+    if (assoc && fuse) return set_error(YOUTH_EINVAL, "launch_reduce: assoc with fused solve");
+    const int sel = (assoc ? 8 : 0) | (fuse ? 4 : 0) | (c->fast ? 2 : 0) | (aligned ? 1 : 0);
     switch (sel) {
-    case 0: launch_reduce_t<false, false, false>(c, s, grid, dsrc, pm, thr2, chunk); break;
-    case 1: launch_reduce_t<false, false, true>(c, s, grid, dsrc, pm, thr2, chunk); break;
-    case 2: launch_reduce_t<false, true, false>(c, s, grid, dsrc, pm, thr2, chunk); break;
-    case 3: launch_reduce_t<false, true, true>(c, s, grid, dsrc, pm, thr2, chunk); break;
-    case 4: launch_reduce_t<true, false, false>(c, s, grid, dsrc, pm, thr2, chunk); break;
-    case 5: launch_reduce_t<true, false, true>(c, s, grid, dsrc, pm, thr2, chunk); break;
-    case 6: launch_reduce_t<true, true, false>(c, s, grid, dsrc, pm, thr2, chunk); break;
-    default: launch_reduce_t<true, true, true>(c, s, grid, dsrc, pm, thr2, chunk); break;
+    case 0: launch_reduce_t<false, false, false, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    case 1: launch_reduce_t<false, false, true, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    case 2: launch_reduce_t<false, true, false, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    case 3: launch_reduce_t<false, true, true, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    case 4: launch_reduce_t<false, false, false, true>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    case 5: launch_reduce_t<false, false, true, true>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    case 6: launch_reduce_t<false, true, false, true>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    case 7: launch_reduce_t<false, true, true, true>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    case 8: launch_reduce_t<true, false, false, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    case 9: launch_reduce_t<true, false, true, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    case 10: launch_reduce_t<true, true, false, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    default: launch_reduce_t<true, true, true, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
     }
     HIP_TRY(hipGetLastError());
     *nblk_out = nb;
@@ -781,17 +889,12 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
     hipLaunchKernelGGL(k_init, dim3((n_pairs + 63) / 64), dim3(64), 0, s, dTi, n_pairs,
                        c->d_T64, c->d_T32, c->d_status);
     HIP_TRY(hipGetLastError());
+    // arrival counters: zeroed every call (G16 "re-initialise every call"),
+    // re-armed in-kernel by each pair's last workgroup between iterations
+    HIP_TRY(hipMemsetAsync(c->d_arrivals, 0, (size_t)c->max_frames * sizeof(unsigned), s));
     for (int it = 0; it < iters; ++it) {
         int nb = 0;
-        rc = launch_reduce(c, s, dsrc, pm, n_pairs, false, &nb);
-        if (rc) return rc;
-        EventPair ep{};
-        rc = ev_begin(c, s, &ep, 1);
-        if (rc) return rc;
-        hipLaunchKernelGGL(k_solve, dim3(n_pairs), dim3(64), 0, s, c->d_partials, nb, it, iters,
-                           c->d_T64, c->d_T32, c->d_status, c->d_stats, (double*)nullptr);
-        HIP_TRY(hipGetLastError());
-        rc = ev_end(c, s, &ep);
+        rc = launch_reduce(c, s, dsrc, pm, n_pairs, false, &nb, it);  // + fused solve
         if (rc) return rc;
     }
     c->last_pairs = n_pairs;
@@ -882,7 +985,7 @@ void youth_icp_destroy(youth_icp_ctx* c)
         }
     void* bufs[] = {c->d_depth, c->d_rec,   c->d_xyz,      c->d_T64, c->d_T32,   c->d_status,
                     c->d_Tinit, c->d_stats, c->d_partials, c->d_neq, c->d_assoc, c->d_Tout,
-                    c->d_flag};
+                    c->d_flag,  c->d_arrivals};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -941,6 +1044,11 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
     if ((e = hipMalloc(&c->d_Tout, MF * 16 * sizeof(float))) != hipSuccess)
         return fail("hipMalloc Tout", e);
     if ((e = hipMalloc(&c->d_flag, 16)) != hipSuccess) return fail("hipMalloc flag", e);
+    const size_t arr_bytes = (MF * sizeof(unsigned) + 15) / 16 * 16;
+    if ((e = hipMalloc(&c->d_arrivals, arr_bytes)) != hipSuccess)
+        return fail("hipMalloc arrivals", e);
+    if ((e = hipMemset(c->d_arrivals, 0, arr_bytes)) != hipSuccess)
+        return fail("memset arrivals", e);
     if ((e = hipDeviceSynchronize()) != hipSuccess) return fail("sync", e);
     if (ensure_stats(c, c->prm.iters > 0 ? c->prm.iters : 1) != YOUTH_OK ||
         verify_fastdiv(c) != YOUTH_OK) {

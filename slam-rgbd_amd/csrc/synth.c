@@ -237,6 +237,8 @@ void youth_synth_pairs(uint64_t base_seed, int first_index, int n, int W, int H,
                        int16_t* dst, double* T_gt)
 {
     const size_t N = (size_t)W * (size_t)H;
+    /* frames are independent (own seeds): parallel over pairs is deterministic */
+#pragma omp parallel for schedule(dynamic, 1)
     for (int p = 0; p < n; ++p)
         youth_synth_pair(base_seed + (uint64_t)(first_index + p), W, H, K, flags,
                          src + (size_t)p * N, dst + (size_t)p * N,
@@ -248,6 +250,7 @@ void youth_synth_sequence(uint64_t seed, int first_frame, int n, int W, int H,
                           double* T_wc)
 {
     const size_t N = (size_t)W * (size_t)H;
+#pragma omp parallel for schedule(dynamic, 1)
     for (int f = 0; f < n; ++f) {
         const int k = first_frame + f;
         const double phi = 0.01 * k;

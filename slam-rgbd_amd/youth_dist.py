@@ -1,0 +1,75 @@
+"""Multi-GPU plumbing for the ICP path: one process per GPU.
+
+* Independent pairs (config C4): rank r owns global pairs [r*n, (r+1)*n);
+  no collective on the data path; the fp32 poses are all-gathered at the end
+  (RCCL over xGMI under the "nccl" backend, gloo in the CPU tests).
+* Streamed sequence (config C5): the F-1 frame pairs (k, k+1) are split into
+  contiguous ranges; rank r also holds the frame after its last pair (a
+  1-frame halo), so no data crosses ranks during tracking.  Rank 0 composes
+  the world trajectory by an ordered fp64 prefix product.
+
+Pure torch.distributed; no device code here.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def pair_shard(rank: int, pairs_per_rank: int) -> tuple[int, int]:
+    """(first global pair index, count) of `rank` under weak scaling."""
+    return rank * pairs_per_rank, pairs_per_rank
+
+
+def sequence_shard(n_frames: int, world: int, rank: int) -> tuple[int, int]:
+    """Frames [f0, f1) held by `rank` so that its pairs (k, k+1), k in
+    [f0, f1-1), tile the F-1 pairs exactly once across ranks; the last frame
+    of each shard is the next shard's first (halo).  Ranks with no pairs get
+    (f, f)."""
+    n_pairs = n_frames - 1
+    base, extra = divmod(n_pairs, world)
+    p0 = rank * base + min(rank, extra)
+    cnt = base + (1 if rank < extra else 0)
+    if cnt == 0:
+        return p0, p0
+    return p0, p0 + cnt + 1
+
+
+def gather_poses(local: torch.Tensor, world: int) -> torch.Tensor:
+    """All-gather [n, 16] pose rows from every rank, rank-ordered."""
+    if world == 1:
+        return local
+    out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
+                      device=local.device)
+    if dist.get_backend() == "nccl":
+        dist.all_gather_into_tensor(out, local.contiguous())
+    else:
+        parts = list(out.chunk(world))
+        dist.all_gather(parts, local.contiguous())
+    return out
+
+
+def gather_ragged(local: torch.Tensor, world: int, max_rows: int) -> torch.Tensor:
+    """All-gather [m_r, 16] rows with different m_r per rank (sequence
+    shards): pad to max_rows, gather counts and rows, strip padding."""
+    if world == 1:
+        return local
+    pad = torch.zeros((max_rows,) + tuple(local.shape[1:]), dtype=local.dtype,
+                      device=local.device)
+    pad[: local.shape[0]] = local
+    cnt = torch.tensor([local.shape[0]], dtype=torch.int64, device=local.device)
+    counts = gather_poses(cnt, world)
+    rows = gather_poses(pad, world).view(world, max_rows, *local.shape[1:])
+    return torch.cat([rows[r, : int(counts[r])] for r in range(world)])
+
+
+def compose_trajectory(rel: np.ndarray) -> np.ndarray:
+    """World poses of frames 0..F-1 from relative poses T_k (P_k = T_k P_{k+1}):
+    T_w,0 = I, T_w,k+1 = T_w,k @ T_k (fp64, ordered)."""
+    rel = np.asarray(rel, dtype=np.float64).reshape(-1, 4, 4)
+    out = np.empty((rel.shape[0] + 1, 4, 4), np.float64)
+    out[0] = np.eye(4)
+    for k in range(rel.shape[0]):
+        out[k + 1] = out[k] @ rel[k]
+    return out
