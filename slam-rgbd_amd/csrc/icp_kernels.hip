@@ -395,11 +395,18 @@ __global__ void k_solve_neq(const double* __restrict__ neq, double* T64, float* 
     }
 }
 
-// T64 <- T_init (or identity), T32 <- float(T64), status <- 0.
+// T64 <- T_init (or identity), T32 <- float(T64), status <- 0; zero the
+// persistent kernel's epoch/arrival words and its dequeue head + error flag
+// (G16: every polled word is re-initialised on every call).
 __global__ void k_init(const double* __restrict__ T_init, int n, double* T64, float* T32,
-                       int32_t* status)
+                       int32_t* status, unsigned* epoch, unsigned* arrivals, int iters,
+                       unsigned* head_err)
 {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p == 0 && head_err) {
+        head_err[0] = 0u;
+        head_err[1] = 0u;
+    }
     if (p >= n) return;
     for (int i = 0; i < 16; ++i) {
         const double v = T_init ? T_init[(size_t)p * 16 + i] : ((i % 5) == 0 ? 1.0 : 0.0);
@@ -407,16 +414,11 @@ __global__ void k_init(const double* __restrict__ T_init, int n, double* T64, fl
         if (i < 12) T32[(size_t)p * 12 + i] = (float)v;
     }
     status[p] = 0;
+    if (epoch) epoch[p] = 0u;
+    if (arrivals)
+        for (int k = 0; k < iters; ++k) arrivals[(size_t)p * iters + k] = 0u;
 }
 
-// [p][16] fp32 4x4 export.
-__global__ void k_export(const double* __restrict__ T64, int n, float* __restrict__ out)
-{
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n * 16) return;
-    const int i = t & 15;
-    out[t] = i < 12 ? (float)T64[(size_t)(t >> 4) * 16 + i] : (i == 15 ? 1.0f : 0.0f);
-}
 
 // ---------------------------------------------------------------- k_reduce --
 // Spec a7-a9 for four consecutive source pixels per lane per step.
@@ -462,29 +464,15 @@ struct PoseState {
     int it, iters;
 };
 
-template <bool kAssoc, bool kFast, bool kAligned, bool kFuse>
-__global__ __launch_bounds__(kRedThreads) void k_reduce(
-    const int16_t* __restrict__ dsrc, const float4* __restrict__ recs, size_t P, PairMap pm,
-    int W, int H, Intr K, FastK F, float thr2, int chunk, double* __restrict__ partials,
-    int32_t* __restrict__ assoc, PoseState ps)
+// Accumulate source pixels [start, end) of one pair into acc (spec a7-a9).
+template <bool kAssoc, bool kFast, bool kAligned>
+__device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
+                                                 const float4* __restrict__ rec,
+                                                 const float* __restrict__ T, int start, int end,
+                                                 int W, int H, const Intr& K, const FastK& F,
+                                                 float thr2, double* acc,
+                                                 int32_t* __restrict__ arow)
 {
-    __shared__ double red[kRedThreads / 64][kNeq];
-    const int p = blockIdx.y;
-    const int b = blockIdx.x;
-    const int N = W * H;
-    const int16_t* sD = dsrc + (size_t)(pm.src0 + p) * N;
-    const float4* rec = recs + (size_t)(pm.tgt0 + p) * P;
-    float T[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) T[k] = ps.T32[p * 12 + k];
-
-    double acc[kNeq];
-#pragma unroll
-    for (int k = 0; k < kNeq; ++k) acc[k] = 0.0;
-
-    const int start = b * chunk;
-    const int end = min(start + chunk, N);
-    int32_t* arow = kAssoc ? assoc + (size_t)p * N : nullptr;
     for (int i = start + threadIdx.x * 4; i < end; i += kRedStep) {
         const short4 d4 = load_depth4<kAligned>(sD, i, end);
         const int dd[4] = {d4.x, d4.y, d4.z, d4.w};
@@ -555,6 +543,33 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce(
         }
     }
 
+}
+
+template <bool kAssoc, bool kFast, bool kAligned, bool kFuse>
+__global__ __launch_bounds__(kRedThreads) void k_reduce(
+    const int16_t* __restrict__ dsrc, const float4* __restrict__ recs, size_t P, PairMap pm,
+    int W, int H, Intr K, FastK F, float thr2, int chunk, double* __restrict__ partials,
+    int32_t* __restrict__ assoc, PoseState ps)
+{
+    __shared__ double red[kRedThreads / 64][kNeq];
+    const int p = blockIdx.y;
+    const int b = blockIdx.x;
+    const int N = W * H;
+    const int16_t* sD = dsrc + (size_t)(pm.src0 + p) * N;
+    const float4* rec = recs + (size_t)(pm.tgt0 + p) * P;
+    float T[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) T[k] = ps.T32[p * 12 + k];
+
+    double acc[kNeq];
+#pragma unroll
+    for (int k = 0; k < kNeq; ++k) acc[k] = 0.0;
+
+    const int start = b * chunk;
+    const int end = min(start + chunk, N);
+    int32_t* arow = kAssoc ? assoc + (size_t)p * N : nullptr;
+    accumulate_chunk<kAssoc, kFast, kAligned>(sD, rec, T, start, end, W, H, K, F, thr2, acc,
+                                              arow);
     // wave butterfly (lane-symmetric: every lane ends with the same sum),
     // then the four waves in fixed order through LDS
 #pragma unroll
@@ -637,6 +652,219 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce(
     }
 }
 
+// ------------------------------------------------------------------- k_icp --
+// ONE persistent launch for all `iters` iterations of a batch.
+//
+// Work item = (iteration k, pair p, chunk c), ordered iteration-major:
+//   item = (k * n_pairs + p) * nblk + c.
+// Workgroups take items from one dynamic dequeue counter.  An item of
+// iteration k >= 1 waits until epoch[p] >= k, i.e. until iteration k-1 of
+// pair p has been solved.  Every item it can wait on has a SMALLER index, so
+// it was dequeued earlier by a running workgroup, and the earliest
+// unfinished item never waits: the scheme cannot deadlock, whatever the
+// residency (no co-residency assumption; cdna_hip_programming.md §1).  Every
+// spin is bounded; a timeout sets *error and the workgroup exits, and the
+// host reports it as YOUTH_STATUS_TIMEOUT (the GPU never hangs).
+//
+// Hand-offs (G16 / MI355X_MICROARCH "Valid forms" row 1): partials, T64 and
+// T32 are written with sc1 stores, the storing wave drains (vmcnt(0)), then
+// ONE agent-scope atomic (arrival ticket) or flag store (epoch); every read
+// of handed-off bytes is an sc1 load by the wave that saw the ticket/flag.
+struct IterState {
+    double* T64;          // [pair][16]
+    float* T32;           // [pair][12]
+    int32_t* status;      // [pair]
+    double* stats;        // [pair][iters][2] or null
+    unsigned* arrivals;   // [pair][iters], zeroed per call
+    unsigned* epoch;      // [pair], zeroed per call
+    unsigned* head;       // dequeue counter, zeroed per call
+    unsigned* error;      // timeout flag, zeroed per call
+    int iters, n_pairs, nblk, chunk;
+};
+
+constexpr unsigned kSpinMax = 1u << 23;  // x s_sleep(8) ~ seconds: a bound, never reached
+
+__device__ __forceinline__ unsigned ld_u32_sc1(const unsigned* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_u64_sc1(const void* p)
+{
+    return __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_u64_sc1(void* p, unsigned long long v)
+{
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), v, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_u32_sc1(void* p, unsigned v)
+{
+    __hip_atomic_store(reinterpret_cast<unsigned*>(p), v, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool kFast, bool kAligned>
+__global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restrict__ dsrc,
+                                                    const float4* __restrict__ recs, size_t P,
+                                                    PairMap pm, int W, int H, Intr K, FastK F,
+                                                    float thr2, double* __restrict__ partials,
+                                                    IterState is)
+{
+    __shared__ double red[kRedThreads / 64][kNeq];
+    __shared__ int sh_item;
+    __shared__ float sh_T[12];
+    const int N = W * H;
+    const int per_iter = is.n_pairs * is.nblk;
+    const int total = is.iters * per_iter;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+
+    for (;;) {
+        if (threadIdx.x == 0) {
+            int item = (int)__hip_atomic_fetch_add(is.head, 1u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+            if (item < total) {
+                const int k = item / per_iter;
+                const int p = (item - k * per_iter) / is.nblk;
+                if (k > 0) {
+                    unsigned spins = 0;
+                    while (ld_u32_sc1(is.epoch + p) < (unsigned)k) {
+                        __builtin_amdgcn_s_sleep(8);
+                        if (++spins > kSpinMax || ld_u32_sc1(is.error) != 0u) {
+                            __hip_atomic_fetch_or(is.error, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+                            item = total;
+                            break;
+                        }
+                    }
+                }
+                if (item < total) {
+                    // the pose of (p, k): sc1 loads after the epoch matched
+#pragma unroll
+                    for (int q = 0; q < 12; q += 2) {
+                        const unsigned long long v = ld_u64_sc1(is.T32 + p * 12 + q);
+                        sh_T[q] = __uint_as_float((unsigned)v);
+                        sh_T[q + 1] = __uint_as_float((unsigned)(v >> 32));
+                    }
+                }
+            }
+            sh_item = item;
+        }
+        __syncthreads();
+        // LDS-broadcast values are wave-uniform: readfirstlane keeps them (and
+        // everything derived from them) in SGPRs, as k_reduce's s_load'ed pose
+        const int item = __builtin_amdgcn_readfirstlane(sh_item);
+        if (item >= total) return;
+        const int k = item / per_iter;
+        const int rem = item - k * per_iter;
+        const int p = rem / is.nblk;
+        const int c = rem - p * is.nblk;
+        float T[12];
+#pragma unroll
+        for (int q = 0; q < 12; ++q)
+            T[q] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sh_T[q])));
+
+        double acc[kNeq];
+#pragma unroll
+        for (int q = 0; q < kNeq; ++q) acc[q] = 0.0;
+        const int start = c * is.chunk;
+        const int end = min(start + is.chunk, N);
+        accumulate_chunk<false, kFast, kAligned>(dsrc + (size_t)(pm.src0 + p) * N,
+                                                 recs + (size_t)(pm.tgt0 + p) * P, T, start,
+                                                 end, W, H, K, F, thr2, acc, nullptr);
+#pragma unroll
+        for (int q = 0; q < kNeq; ++q) {
+            double v = acc[q];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+            acc[q] = v;
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int q = 0; q < kNeq; ++q) red[wave][q] = acc[q];
+        }
+        __syncthreads();
+        if (wave != 0) continue;  // waves 1-3: next item (wait at its barrier)
+
+        // ---- wave 0: publish this chunk's partial, take the arrival ticket
+        double sum = 0.0;
+        if (lane < kNeq) {
+#pragma unroll
+            for (int w = 0; w < kRedThreads / 64; ++w) sum += red[w][lane];
+            st_u64_sc1(partials + ((size_t)p * is.nblk + c) * kNeq + lane,
+                       (unsigned long long)__double_as_longlong(sum));
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned ticket = 0;
+        if (lane == 0)
+            ticket = __hip_atomic_fetch_add(is.arrivals + (size_t)p * is.iters + k, 1u,
+                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ticket = __shfl(ticket, 0, 64);
+        if (ticket != (unsigned)is.nblk - 1) continue;
+
+        // ---- last arriver of (p, k): fixed-order sum (as k_solve), solve,
+        // publish the pose, then the epoch
+        const double* base = partials + (size_t)p * is.nblk * kNeq;
+        const int half = (is.nblk + 1) >> 1;
+        const int kk = lane & 31;
+        double t = 0.0;
+        if (kk < kNeq) {
+            const int b0 = lane < 32 ? 0 : half;
+            const int b1 = lane < 32 ? half : is.nblk;
+            for (int bb = b0; bb < b1; bb += 8) {
+                double v[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    v[q] = bb + q < b1
+                               ? __longlong_as_double((long long)ld_u64_sc1(
+                                     base + (size_t)(bb + q) * kNeq + kk))
+                               : 0.0;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) t += v[q];
+            }
+        }
+        t += __shfl_down(t, 32, 64);
+        double neq[kNeq];
+#pragma unroll
+        for (int q = 0; q < kNeq; ++q) neq[q] = __shfl(t, q, 64);
+        if (lane == 0) {
+            if (is.stats) {
+                is.stats[((size_t)p * is.iters + k) * 2 + 0] = neq[28];
+                is.stats[((size_t)p * is.iters + k) * 2 + 1] = neq[27];
+            }
+            double xi[6];
+            const int st = solve6(neq, xi);  // before the pose loads: shorter live ranges
+            double Tm[16];
+            for (int q = 0; q < 12; ++q)
+                Tm[q] = __longlong_as_double((long long)ld_u64_sc1(is.T64 + (size_t)p * 16 + q));
+            if (st == 0) se3_exp_left(xi, Tm);
+            if (st) __hip_atomic_fetch_or(is.status + p, st, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+            for (int q = 0; q < 12; ++q)
+                st_u64_sc1(is.T64 + (size_t)p * 16 + q, (unsigned long long)__double_as_longlong(Tm[q]));
+            for (int q = 0; q < 12; q += 2)
+                st_u64_sc1(is.T32 + (size_t)p * 12 + q,
+                           (unsigned long long)__float_as_uint((float)Tm[q]) |
+                               ((unsigned long long)__float_as_uint((float)Tm[q + 1]) << 32));
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            st_u32_sc1(is.epoch + p, (unsigned)(k + 1));
+        }
+    }
+}
+
+// Copy out fp32 4x4 poses (optional) and fold a persistent-kernel timeout
+// into every pair's status.
+__global__ void k_finish(const double* __restrict__ T64, int n, float* __restrict__ out,
+                         int32_t* __restrict__ status, const unsigned* __restrict__ error)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * 16) return;
+    const int i = t & 15;
+    if (out) out[t] = i < 12 ? (float)T64[(size_t)(t >> 4) * 16 + i] : (i == 15 ? 1.0f : 0.0f);
+    if (i == 0 && error && *error) status[t >> 4] |= YOUTH_STATUS_TIMEOUT;
+}
+
 }  // namespace
 
 // =============================================================== host side ==
@@ -693,6 +921,12 @@ struct youth_icp_ctx {
     float* d_Tout = nullptr;  // [max_frames][16]
     unsigned* d_flag = nullptr;
     unsigned* d_arrivals = nullptr;  // [max_frames] fused-solve arrival counters
+    unsigned* d_arr_it = nullptr;    // [max_frames][stats_iters] persistent arrival tickets
+    unsigned* d_epoch = nullptr;     // [max_frames] persistent pose epochs
+    unsigned* d_head = nullptr;      // [4]: dequeue head, timeout flag
+    bool persistent = true;          // one k_icp launch per align (else per-iteration k_reduce)
+    int icp_blocks_per_cu[4] = {0, 0, 0, 0};  // occupancy of k_icp<fast, aligned>
+    int n_cu = 0;
 
     int last_pairs = 0;
     int last_iters = 0;
@@ -709,9 +943,13 @@ struct youth_icp_ctx {
 
 static int reduce_geometry(const youth_icp_ctx* c, int n_pairs, int* chunk_out)
 {
-    // ~2048 workgroups per launch (tools/kbench: best of 1024/2048/4096 at
-    // 64 pairs), at least 8 pixels per lane.
-    const int target_blocks = 2048;
+    // ~2048 work chunks per iteration (tools/kbench: best of 1024/2048/4096
+    // at 64 pairs), at least 8 pixels per lane.
+    static const int target_blocks = [] {
+        const char* e = getenv("YOUTH_ICP_TARGET_CHUNKS");  // tuning knob
+        const int v = e ? atoi(e) : 0;
+        return v > 0 ? v : 2048;
+    }();
     int nb = (target_blocks + n_pairs - 1) / n_pairs;
     const int max_nb = (c->N + 2 * kRedStep - 1) / (2 * kRedStep);
     if (nb > max_nb) nb = max_nb;
@@ -738,8 +976,11 @@ static int ensure_stats(youth_icp_ctx* c, int iters)
 {
     if (iters <= c->stats_iters) return YOUTH_OK;
     if (c->d_stats) HIP_TRY(hipFree(c->d_stats));
+    if (c->d_arr_it) HIP_TRY(hipFree(c->d_arr_it));
     c->d_stats = nullptr;
+    c->d_arr_it = nullptr;
     HIP_TRY(hipMalloc(&c->d_stats, (size_t)c->max_frames * iters * 2 * sizeof(double)));
+    HIP_TRY(hipMalloc(&c->d_arr_it, (size_t)c->max_frames * iters * sizeof(unsigned)));
     c->stats_iters = iters;
     return YOUTH_OK;
 }
@@ -886,16 +1127,43 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
                                hipMemcpyHostToDevice, s));
         dTi = c->d_Tinit;
     }
-    hipLaunchKernelGGL(k_init, dim3((n_pairs + 63) / 64), dim3(64), 0, s, dTi, n_pairs,
-                       c->d_T64, c->d_T32, c->d_status);
+    const bool persistent = c->persistent && iters > 0;
+    hipLaunchKernelGGL(k_init, dim3((n_pairs + 63) / 64), dim3(64), 0, s, dTi, n_pairs, c->d_T64,
+                       c->d_T32, c->d_status, persistent ? c->d_epoch : (unsigned*)nullptr,
+                       persistent ? c->d_arr_it : (unsigned*)nullptr, iters, c->d_head);
     HIP_TRY(hipGetLastError());
-    // arrival counters: zeroed every call (G16 "re-initialise every call"),
-    // re-armed in-kernel by each pair's last workgroup between iterations
-    HIP_TRY(hipMemsetAsync(c->d_arrivals, 0, (size_t)c->max_frames * sizeof(unsigned), s));
-    for (int it = 0; it < iters; ++it) {
-        int nb = 0;
-        rc = launch_reduce(c, s, dsrc, pm, n_pairs, false, &nb, it);  // + fused solve
+    if (persistent) {
+        int chunk = 0;
+        const int nb = reduce_geometry(c, n_pairs, &chunk);
+        rc = ensure_partials(c, (size_t)nb * n_pairs * kNeq);
         if (rc) return rc;
+        const bool aligned = (reinterpret_cast<uintptr_t>(dsrc) % 8 == 0) && (c->N % 4 == 0);
+        const int var = (c->fast ? 2 : 0) | (aligned ? 1 : 0);
+        const long long items = (long long)iters * n_pairs * nb;
+        long long grid = (long long)c->n_cu * c->icp_blocks_per_cu[var];
+        if (grid > items) grid = items;
+        if (grid < 1) grid = 1;
+        const IterState is{c->d_T64, c->d_T32, c->d_status, c->d_stats, c->d_arr_it, c->d_epoch,
+                           c->d_head, c->d_head + 1, iters, n_pairs, nb, chunk};
+        const float thr2 = c->prm.dist_thresh * c->prm.dist_thresh;
+        EventPair ep{};
+        rc = ev_begin(c, s, &ep, 0);
+        if (rc) return rc;
+        auto kern = c->fast ? (aligned ? k_icp<true, true> : k_icp<true, false>)
+                            : (aligned ? k_icp<false, true> : k_icp<false, false>);
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kRedThreads), 0, s, dsrc, c->d_rec,
+                           c->P, pm, c->W, c->H, c->K, c->F, thr2, c->d_partials, is);
+        HIP_TRY(hipGetLastError());
+        rc = ev_end(c, s, &ep);
+        if (rc) return rc;
+    } else {
+        // arrival counters of the per-iteration fused kernel, re-armed in-kernel
+        HIP_TRY(hipMemsetAsync(c->d_arrivals, 0, (size_t)c->max_frames * sizeof(unsigned), s));
+        for (int it = 0; it < iters; ++it) {
+            int nb = 0;
+            rc = launch_reduce(c, s, dsrc, pm, n_pairs, false, &nb, it);  // + fused solve
+            if (rc) return rc;
+        }
     }
     c->last_pairs = n_pairs;
     c->last_iters = iters;
@@ -905,9 +1173,8 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
 
 static int export_poses(youth_icp_ctx* c, hipStream_t s, int n_pairs, float* d_T_out)
 {
-    if (!d_T_out) return YOUTH_OK;
-    hipLaunchKernelGGL(k_export, dim3((n_pairs * 16 + 255) / 256), dim3(256), 0, s, c->d_T64,
-                       n_pairs, d_T_out);
+    hipLaunchKernelGGL(k_finish, dim3((n_pairs * 16 + 255) / 256), dim3(256), 0, s, c->d_T64,
+                       n_pairs, d_T_out, c->d_status, (const unsigned*)(c->d_head + 1));
     HIP_TRY(hipGetLastError());
     return YOUTH_OK;
 }
@@ -985,7 +1252,7 @@ void youth_icp_destroy(youth_icp_ctx* c)
         }
     void* bufs[] = {c->d_depth, c->d_rec,   c->d_xyz,      c->d_T64, c->d_T32,   c->d_status,
                     c->d_Tinit, c->d_stats, c->d_partials, c->d_neq, c->d_assoc, c->d_Tout,
-                    c->d_flag,  c->d_arrivals};
+                    c->d_flag,  c->d_arrivals, c->d_arr_it, c->d_epoch, c->d_head};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1044,6 +1311,27 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
     if ((e = hipMalloc(&c->d_Tout, MF * 16 * sizeof(float))) != hipSuccess)
         return fail("hipMalloc Tout", e);
     if ((e = hipMalloc(&c->d_flag, 16)) != hipSuccess) return fail("hipMalloc flag", e);
+    if ((e = hipMalloc(&c->d_epoch, MF * sizeof(unsigned))) != hipSuccess)
+        return fail("hipMalloc epoch", e);
+    if ((e = hipMalloc(&c->d_head, 16)) != hipSuccess) return fail("hipMalloc head", e);
+    if ((e = hipMemset(c->d_head, 0, 16)) != hipSuccess) return fail("memset head", e);
+    {
+        hipDeviceProp_t prop;
+        if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess)
+            return fail("hipGetDeviceProperties", e);
+        c->n_cu = prop.multiProcessorCount;
+        const void* kerns[4] = {(const void*)k_icp<false, false>, (const void*)k_icp<false, true>,
+                                (const void*)k_icp<true, false>, (const void*)k_icp<true, true>};
+        for (int v = 0; v < 4; ++v) {
+            int nb = 0;
+            if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kerns[v], kRedThreads, 0)) !=
+                hipSuccess)
+                return fail("occupancy", e);
+            c->icp_blocks_per_cu[v] = nb > 0 ? nb : 1;
+        }
+        const char* np = getenv("YOUTH_ICP_NO_PERSISTENT");
+        c->persistent = !(np && *np && *np != '0');
+    }
     const size_t arr_bytes = (MF * sizeof(unsigned) + 15) / 16 * 16;
     if ((e = hipMalloc(&c->d_arrivals, arr_bytes)) != hipSuccess)
         return fail("hipMalloc arrivals", e);
