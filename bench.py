@@ -166,6 +166,8 @@ def run_pairs(R):
     }
     result["roofline"] = R.roofline(kt, n * W * H)
     result["kernel_ms_per_step"] = {k: v[0] / a.steps for k, v in kt.items()}
+    spins, waited = ctx.get_sched_stats()   # last align: persistent-kernel pose waits
+    result["sched_last_step"] = {"epoch_polls": spins, "items_waited": waited}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         result["cpu_baseline"], result["parity"] = cpu_baseline(a, src, dst, T_gpu)
     ctx.close()

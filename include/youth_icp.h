@@ -186,6 +186,13 @@ int youth_icp_set_timing(youth_icp_ctx* ctx, int enable);
 int youth_icp_get_timing(youth_icp_ctx* ctx, int kind, double* total_ms,
                          int* launches);
 
+/* Scheduler telemetry of the LAST persistent align on this context: total
+ * epoch polls (each followed by s_sleep 8) and the number of work items that
+ * had to wait for their pair's previous-iteration pose.  Synchronises the
+ * context stream.  Zero for the per-iteration (non-persistent) path. */
+int youth_icp_get_sched_stats(youth_icp_ctx* ctx, unsigned* spins,
+                              unsigned* waited_items);
+
 /* --- Stage-level entry points (validation / parity tests) --------------- */
 
 /* Depth -> XYZ planes (+ normals when want_normals) for n_frames host frames.

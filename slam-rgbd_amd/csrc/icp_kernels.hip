@@ -58,6 +58,9 @@ constexpr int kLdsH = kTileH + 2;
 constexpr int kRedThreads = 256;
 constexpr int kRedStep = kRedThreads * 4;  // pixels per workgroup loop step
 constexpr int kNeq = YOUTH_NEQ;
+// Persistent-queue words (unsigned index into ctx->d_head), one 128-B line
+// apart so the contended dequeue atomic shares no line with the polled flag.
+constexpr int kQHead = 0, kQError = 32, kQSpins = 64, kQWaited = 96, kQWords = 128;
 
 struct Intr {
     float fx, fy, cx, cy, ds;
@@ -403,9 +406,11 @@ __global__ void k_init(const double* __restrict__ T_init, int n, double* T64, fl
                        unsigned* head_err)
 {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p == 0 && head_err) {
-        head_err[0] = 0u;
-        head_err[1] = 0u;
+    if (p == 0 && head_err) {  // one 128-B line each (kQ*): no false sharing
+        head_err[kQHead] = 0u;     // dequeue head (contended atomic)
+        head_err[kQError] = 0u;    // timeout flag (polled by waiters)
+        head_err[kQSpins] = 0u;    // epoch polls (scheduler telemetry)
+        head_err[kQWaited] = 0u;   // items that had to wait for their pair's pose
     }
     if (p >= n) return;
     for (int i = 0; i < 16; ++i) {
@@ -423,7 +428,7 @@ __global__ void k_init(const double* __restrict__ T_init, int n, double* T64, fl
 // ---------------------------------------------------------------- k_reduce --
 // Spec a7-a9 for four consecutive source pixels per lane per step.
 //   source  int16 depth (2 B/px), back-projected in registers (8-byte load
-//           per lane when the frame is 8-byte aligned and N % 4 == 0);
+//           per lane when the frame is 8-byte aligned and W % 4 == 0);
 //   target  ONE aligned 16-byte record fetch {z, nx, ny, nz} per pixel; the
 //           target's x, y are recomputed from z with k_prep's expression, so
 //           they are bit-identical to what k_prep would have stored.
@@ -473,39 +478,56 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
                                                  float thr2, double* acc,
                                                  int32_t* __restrict__ arow)
 {
-    for (int i = start + threadIdx.x * 4; i < end; i += kRedStep) {
+    // (u0, v0) of pixel i advance incrementally (no integer division per
+    // step); with kAligned (W % 4 == 0, i % 4 == 0) a lane's four pixels
+    // share one row.  Conditions combine with '&' so the compiler emits
+    // selects, not exec-mask branches; unmatched pixels gather record 0 and
+    // are masked.
+    const int stepV = kRedStep / W;
+    const int stepU = kRedStep - stepV * W;
+    int i = start + threadIdx.x * 4;
+    int v0 = i / W;
+    int u0 = i - v0 * W;
+    int cnt = 0;
+    for (; i < end; i += kRedStep) {
         const short4 d4 = load_depth4<kAligned>(sD, i, end);
         const int dd[4] = {d4.x, d4.y, d4.z, d4.w};
-        const int v0 = i / W;
-        const int u0 = i - v0 * W;
         // spec a7: P' = R P + t (fixed order, no FMA); projective association
         float qx[4], qy[4], qz[4], fu[4], fv[4];
+        bool in[4];
         int j[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             int u = u0 + q, v = v0;
-            if (u >= W) {
-                u -= W;
-                ++v;
+            if (!kAligned) {
+                const bool wrap = u >= W;
+                u = wrap ? u - W : u;
+                v = wrap ? v + 1 : v;
             }
             float sx, sy, sz;
-            backproject<kFast>((i + q) < end ? dd[q] : 0, u, v, K, F, sx, sy, sz);
+            backproject<kFast>(kAligned || (i + q) < end ? dd[q] : 0, u, v, K, F, sx, sy, sz);
             qx[q] = ((T[0] * sx + T[1] * sy) + T[2] * sz) + T[3];
             qy[q] = ((T[4] * sx + T[5] * sy) + T[6] * sz) + T[7];
             qz[q] = ((T[8] * sx + T[9] * sy) + T[10] * sz) + T[11];
-            const bool vz = sz > 0.0f && qz[q] > 0.0f;
+            const bool vz = (sz > 0.0f) & (qz[q] > 0.0f);
             const float qzs = vz ? qz[q] : 1.0f;
             const float uu = floorf((((K.fx * qx[q]) / qzs) + K.cx) + 0.5f);
             const float vv = floorf((((K.fy * qy[q]) / qzs) + K.cy) + 0.5f);
-            const bool in = vz && uu >= 0.0f && uu < (float)W && vv >= 0.0f && vv < (float)H;
-            fu[q] = in ? uu : 0.0f;
-            fv[q] = in ? vv : 0.0f;
-            j[q] = in ? (int)fv[q] * W + (int)fu[q] : -1;
+            in[q] = vz & (uu >= 0.0f) & (uu < (float)W) & (vv >= 0.0f) & (vv < (float)H);
+            fu[q] = in[q] ? uu : 0.0f;
+            fv[q] = in[q] ? vv : 0.0f;
+            j[q] = (int)fv[q] * W + (int)fu[q];  // 0 when !in
         }
-        // four 16-byte fetches back to back (clamped index: no branch)
+        u0 += stepU;
+        v0 += stepV;
+        if (u0 >= W) {
+            u0 -= W;
+            ++v0;
+        }
+        // four 16-byte fetches back to back
         float4 t[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) t[q] = rec[j[q] >= 0 ? j[q] : 0];
+        for (int q = 0; q < 4; ++q) t[q] = rec[j[q]];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const float tz = t[q].x;
@@ -514,8 +536,8 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
             const float nx = t[q].y, ny = t[q].z, nz = t[q].w;
             const float dx = qx[q] - tx, dy = qy[q] - ty, dz = qz[q] - tz;
             const float d2 = (dx * dx + dy * dy) + dz * dz;
-            const bool nvalid = !(nx == 0.0f && ny == 0.0f && nz == 0.0f);
-            const bool ok = j[q] >= 0 && tz > 0.0f && nvalid && d2 < thr2;
+            const bool nvalid = (nx != 0.0f) | (ny != 0.0f) | (nz != 0.0f);
+            const bool ok = in[q] & (tz > 0.0f) & nvalid & (d2 < thr2);
             if (kAssoc && (i + q) < end) arow[i + q] = ok ? j[q] : -1;
             // spec a8: r = n.(P' - P_t); J = [P' x n, n]  (zeros when unmatched)
             const float n0 = ok ? nx : 0.0f, n1 = ok ? ny : 0.0f, n2 = ok ? nz : 0.0f;
@@ -539,10 +561,37 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
 #pragma unroll
             for (int a = 0; a < 6; ++a) acc[21 + a] = fma((double)Jf[a], (double)r, acc[21 + a]);
             acc[27] = fma((double)r, (double)r, acc[27]);
-            acc[28] += ok ? 1.0 : 0.0;
+            cnt += ok ? 1 : 0;
         }
     }
+    acc[28] += (double)cnt;
+}
 
+// Wave sum of the kNeq per-lane accumulators by recursive halving: at lane
+// mask m = 32, 16, 8, 4, 2 each lane keeps one half of its remaining values
+// (the upper half iff lane & m) and sends the other half to lane ^ m, so the
+// fp64 exchanges number 16 + 8 + 4 + 2 + 1 + 1 = 32 instead of 29 x 6 for a
+// symmetric butterfly.  On exit lane 2q and 2q+1 both hold the wave total of
+// value q (q < kNeq); the summation tree is fixed, so results are
+// deterministic.  Shared by k_reduce and k_icp.
+__device__ __forceinline__ void wave_reduce_scatter(const double* acc, int lane, double& total)
+{
+    double v[32];
+#pragma unroll
+    for (int q = 0; q < 32; ++q) v[q] = q < kNeq ? acc[q] : 0.0;
+#pragma unroll
+    for (int st = 0; st < 5; ++st) {
+        const int m = 32 >> st;
+        const int h = 16 >> st;
+        const bool up = (lane & m) != 0;
+#pragma unroll
+        for (int q = 0; q < h; ++q) {
+            const double send = up ? v[q] : v[q + h];
+            const double keep = up ? v[q + h] : v[q];
+            v[q] = keep + __shfl_xor(send, m, 64);
+        }
+    }
+    total = v[0] + __shfl_xor(v[0], 1, 64);
 }
 
 template <bool kAssoc, bool kFast, bool kAligned, bool kFuse>
@@ -570,19 +619,13 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce(
     int32_t* arow = kAssoc ? assoc + (size_t)p * N : nullptr;
     accumulate_chunk<kAssoc, kFast, kAligned>(sD, rec, T, start, end, W, H, K, F, thr2, acc,
                                               arow);
-    // wave butterfly (lane-symmetric: every lane ends with the same sum),
-    // then the four waves in fixed order through LDS
-#pragma unroll
-    for (int k = 0; k < kNeq; ++k) {
-        double v = acc[k];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-        acc[k] = v;
-    }
+    // wave reduce-scatter, then the four waves in fixed order through LDS
     const int wave = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-        for (int k = 0; k < kNeq; ++k) red[wave][k] = acc[k];
+    {
+        const int ln = threadIdx.x & 63;
+        double tot;
+        wave_reduce_scatter(acc, ln, tot);
+        if (!(ln & 1) && (ln >> 1) < kNeq) red[wave][ln >> 1] = tot;
     }
     __syncthreads();
     if (threadIdx.x >= 64) return;  // wave 0 publishes (and, if last, solves)
@@ -704,6 +747,55 @@ __device__ __forceinline__ void st_u32_sc1(void* p, unsigned v)
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Queue side of a work item, run by thread 0 after its workgroup published
+// its previous partial (so a waiting workgroup never holds work another one
+// waits for): wait (bounded) until pair p's pose epoch reaches k, then copy
+// the pose into LDS.  Returns the item, or `total` when the queue is drained
+// or after a timeout (error flag set).
+__device__ __forceinline__ int icp_claim(const IterState& is, int item, int total, int per_iter,
+                                         float* sh_T)
+{
+    if (item >= total) return total;
+    const int k = item / per_iter;
+    const int p = (item - k * per_iter) / is.nblk;
+    if (k > 0) {
+        unsigned spins = 0;
+        while (ld_u32_sc1(is.epoch + p) < (unsigned)k) {
+            __builtin_amdgcn_s_sleep(8);
+            if (++spins > kSpinMax || ld_u32_sc1(is.error) != 0u) {
+                __hip_atomic_fetch_or(is.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return total;
+            }
+        }
+        if (spins) {  // scheduler telemetry (youth_icp_get_sched_stats)
+            __hip_atomic_fetch_add(is.head + (kQSpins - kQHead), spins, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(is.head + (kQWaited - kQHead), 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    // the pose of (p, k): sc1 loads after the epoch matched
+    unsigned long long v[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) v[q] = ld_u64_sc1(is.T32 + p * 12 + 2 * q);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        sh_T[2 * q] = __uint_as_float((unsigned)v[q]);
+        sh_T[2 * q + 1] = __uint_as_float((unsigned)(v[q] >> 32));
+    }
+    return item;
+}
+
+// Persistent ICP: ONE launch runs every iteration of every pair.  Work items
+// (k, p, c) = (iteration, pair, pixel chunk) are dequeued in that order from
+// one agent-scope counter; item (k, p, c) needs pair p's pose after k
+// updates, published by the LAST workgroup to finish a chunk of (p, k-1)
+// (arrival ticket), which sums the pair's partials in fixed order, solves and
+// bumps epoch[p].  Per item: pixel loop -> wave reduce-scatter -> barrier ->
+// wave 0 publishes the partial, takes the ticket (and, if last, solves) ->
+// thread 0 dequeues and claims the next item -> barrier.
+// (Dequeuing ahead from wave 1 so that waves 1-3 skip the second barrier
+// measured no faster: DESIGN.md §5.)
 template <bool kFast, bool kAligned>
 __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restrict__ dsrc,
                                                     const float4* __restrict__ recs, size_t P,
@@ -720,40 +812,15 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
 
+    if (threadIdx.x == 0) {
+        const int first = (int)__hip_atomic_fetch_add(is.head, 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+        sh_item = icp_claim(is, first, total, per_iter, sh_T);
+    }
+    __syncthreads();
     for (;;) {
-        if (threadIdx.x == 0) {
-            int item = (int)__hip_atomic_fetch_add(is.head, 1u, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
-            if (item < total) {
-                const int k = item / per_iter;
-                const int p = (item - k * per_iter) / is.nblk;
-                if (k > 0) {
-                    unsigned spins = 0;
-                    while (ld_u32_sc1(is.epoch + p) < (unsigned)k) {
-                        __builtin_amdgcn_s_sleep(8);
-                        if (++spins > kSpinMax || ld_u32_sc1(is.error) != 0u) {
-                            __hip_atomic_fetch_or(is.error, 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-                            item = total;
-                            break;
-                        }
-                    }
-                }
-                if (item < total) {
-                    // the pose of (p, k): sc1 loads after the epoch matched
-#pragma unroll
-                    for (int q = 0; q < 12; q += 2) {
-                        const unsigned long long v = ld_u64_sc1(is.T32 + p * 12 + q);
-                        sh_T[q] = __uint_as_float((unsigned)v);
-                        sh_T[q + 1] = __uint_as_float((unsigned)(v >> 32));
-                    }
-                }
-            }
-            sh_item = item;
-        }
-        __syncthreads();
-        // LDS-broadcast values are wave-uniform: readfirstlane keeps them (and
-        // everything derived from them) in SGPRs, as k_reduce's s_load'ed pose
+        // LDS-broadcast values are wave-uniform: readfirstlane keeps them
+        // (and everything derived from them) in SGPRs
         const int item = __builtin_amdgcn_readfirstlane(sh_item);
         if (item >= total) return;
         const int k = item / per_iter;
@@ -773,83 +840,92 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
         accumulate_chunk<false, kFast, kAligned>(dsrc + (size_t)(pm.src0 + p) * N,
                                                  recs + (size_t)(pm.tgt0 + p) * P, T, start,
                                                  end, W, H, K, F, thr2, acc, nullptr);
-#pragma unroll
-        for (int q = 0; q < kNeq; ++q) {
-            double v = acc[q];
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-            acc[q] = v;
-        }
-        if (lane == 0) {
-#pragma unroll
-            for (int q = 0; q < kNeq; ++q) red[wave][q] = acc[q];
+        {
+            double tot;
+            wave_reduce_scatter(acc, lane, tot);
+            if (!(lane & 1) && (lane >> 1) < kNeq) red[wave][lane >> 1] = tot;
         }
         __syncthreads();
-        if (wave != 0) continue;  // waves 1-3: next item (wait at its barrier)
 
-        // ---- wave 0: publish this chunk's partial, take the arrival ticket
-        double sum = 0.0;
-        if (lane < kNeq) {
+        if (wave == 0) {
+            // ---- publish this chunk's partial, take the arrival ticket
+            double sum = 0.0;
+            if (lane < kNeq) {
 #pragma unroll
-            for (int w = 0; w < kRedThreads / 64; ++w) sum += red[w][lane];
-            st_u64_sc1(partials + ((size_t)p * is.nblk + c) * kNeq + lane,
-                       (unsigned long long)__double_as_longlong(sum));
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        unsigned ticket = 0;
-        if (lane == 0)
-            ticket = __hip_atomic_fetch_add(is.arrivals + (size_t)p * is.iters + k, 1u,
-                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ticket = __shfl(ticket, 0, 64);
-        if (ticket != (unsigned)is.nblk - 1) continue;
-
-        // ---- last arriver of (p, k): fixed-order sum (as k_solve), solve,
-        // publish the pose, then the epoch
-        const double* base = partials + (size_t)p * is.nblk * kNeq;
-        const int half = (is.nblk + 1) >> 1;
-        const int kk = lane & 31;
-        double t = 0.0;
-        if (kk < kNeq) {
-            const int b0 = lane < 32 ? 0 : half;
-            const int b1 = lane < 32 ? half : is.nblk;
-            for (int bb = b0; bb < b1; bb += 8) {
-                double v[8];
-#pragma unroll
-                for (int q = 0; q < 8; ++q)
-                    v[q] = bb + q < b1
-                               ? __longlong_as_double((long long)ld_u64_sc1(
-                                     base + (size_t)(bb + q) * kNeq + kk))
-                               : 0.0;
-#pragma unroll
-                for (int q = 0; q < 8; ++q) t += v[q];
+                for (int w = 0; w < kRedThreads / 64; ++w) sum += red[w][lane];
+                st_u64_sc1(partials + ((size_t)p * is.nblk + c) * kNeq + lane,
+                           (unsigned long long)__double_as_longlong(sum));
             }
-        }
-        t += __shfl_down(t, 32, 64);
-        double neq[kNeq];
-#pragma unroll
-        for (int q = 0; q < kNeq; ++q) neq[q] = __shfl(t, q, 64);
-        if (lane == 0) {
-            if (is.stats) {
-                is.stats[((size_t)p * is.iters + k) * 2 + 0] = neq[28];
-                is.stats[((size_t)p * is.iters + k) * 2 + 1] = neq[27];
-            }
-            double xi[6];
-            const int st = solve6(neq, xi);  // before the pose loads: shorter live ranges
-            double Tm[16];
-            for (int q = 0; q < 12; ++q)
-                Tm[q] = __longlong_as_double((long long)ld_u64_sc1(is.T64 + (size_t)p * 16 + q));
-            if (st == 0) se3_exp_left(xi, Tm);
-            if (st) __hip_atomic_fetch_or(is.status + p, st, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-            for (int q = 0; q < 12; ++q)
-                st_u64_sc1(is.T64 + (size_t)p * 16 + q, (unsigned long long)__double_as_longlong(Tm[q]));
-            for (int q = 0; q < 12; q += 2)
-                st_u64_sc1(is.T32 + (size_t)p * 12 + q,
-                           (unsigned long long)__float_as_uint((float)Tm[q]) |
-                               ((unsigned long long)__float_as_uint((float)Tm[q + 1]) << 32));
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            st_u32_sc1(is.epoch + p, (unsigned)(k + 1));
+            unsigned ticket = 0;
+            if (lane == 0)
+                ticket = __hip_atomic_fetch_add(is.arrivals + (size_t)p * is.iters + k, 1u,
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ticket = __shfl(ticket, 0, 64);
+            if (ticket == (unsigned)is.nblk - 1) {
+                // ---- last arriver of (p, k): fixed-order sum (as k_solve),
+                // solve, publish the pose, then the epoch.  The fp64 pose
+                // (lanes 32..43) is loaded with the partials (batches of 16).
+                const double* base = partials + (size_t)p * is.nblk * kNeq;
+                const int half = (is.nblk + 1) >> 1;
+                const int kk = lane & 31;
+                double Tl = 0.0;
+                if (lane >= 32 && lane < 44)
+                    Tl = __longlong_as_double(
+                        (long long)ld_u64_sc1(is.T64 + (size_t)p * 16 + (lane - 32)));
+                double t = 0.0;
+                if (kk < kNeq) {
+                    const int b0 = lane < 32 ? 0 : half;
+                    const int b1 = lane < 32 ? half : is.nblk;
+                    for (int bb = b0; bb < b1; bb += 16) {
+                        double v[16];
+#pragma unroll
+                        for (int q = 0; q < 16; ++q)
+                            v[q] = bb + q < b1
+                                       ? __longlong_as_double((long long)ld_u64_sc1(
+                                             base + (size_t)(bb + q) * kNeq + kk))
+                                       : 0.0;
+#pragma unroll
+                        for (int q = 0; q < 16; ++q) t += v[q];
+                    }
+                }
+                t += __shfl_down(t, 32, 64);
+                double neq[kNeq];
+#pragma unroll
+                for (int q = 0; q < kNeq; ++q) neq[q] = __shfl(t, q, 64);
+                double Tm[16];
+#pragma unroll
+                for (int q = 0; q < 12; ++q) Tm[q] = __shfl(Tl, 32 + q, 64);
+                if (lane == 0) {
+                    if (is.stats) {
+                        is.stats[((size_t)p * is.iters + k) * 2 + 0] = neq[28];
+                        is.stats[((size_t)p * is.iters + k) * 2 + 1] = neq[27];
+                    }
+                    double xi[6];
+                    const int st = solve6(neq, xi);
+                    if (st == 0) se3_exp_left(xi, Tm);
+                    if (st) __hip_atomic_fetch_or(is.status + p, st, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+                    for (int q = 0; q < 12; ++q)
+                        st_u64_sc1(is.T64 + (size_t)p * 16 + q,
+                                   (unsigned long long)__double_as_longlong(Tm[q]));
+                    for (int q = 0; q < 12; q += 2)
+                        st_u64_sc1(is.T32 + (size_t)p * 12 + q,
+                                   (unsigned long long)__float_as_uint((float)Tm[q]) |
+                                       ((unsigned long long)__float_as_uint((float)Tm[q + 1])
+                                        << 32));
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    st_u32_sc1(is.epoch + p, (unsigned)(k + 1));
+                }
+            }
+            // ---- next item (this workgroup has published: waiting is safe)
+            if (lane == 0) {
+                const int next = (int)__hip_atomic_fetch_add(is.head, 1u, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT);
+                sh_item = icp_claim(is, next, total, per_iter, sh_T);
+            }
         }
+        __syncthreads();
     }
 }
 
@@ -923,7 +999,7 @@ struct youth_icp_ctx {
     unsigned* d_arrivals = nullptr;  // [max_frames] fused-solve arrival counters
     unsigned* d_arr_it = nullptr;    // [max_frames][stats_iters] persistent arrival tickets
     unsigned* d_epoch = nullptr;     // [max_frames] persistent pose epochs
-    unsigned* d_head = nullptr;      // [4]: dequeue head, timeout flag
+    unsigned* d_head = nullptr;      // queue words kQHead / kQError / kQSpins / kQWaited
     bool persistent = true;          // one k_icp launch per align (else per-iteration k_reduce)
     int icp_blocks_per_cu[4] = {0, 0, 0, 0};  // occupancy of k_icp<fast, aligned>
     int n_cu = 0;
@@ -943,12 +1019,13 @@ struct youth_icp_ctx {
 
 static int reduce_geometry(const youth_icp_ctx* c, int n_pairs, int* chunk_out)
 {
-    // ~2048 work chunks per iteration (tools/kbench: best of 1024/2048/4096
-    // at 64 pairs), at least 8 pixels per lane.
+    // ~3072 work chunks per iteration (persistent kernel at 64 pairs: best of
+    // 1536..4096; fewer chunks make items wait for their pair's pose, more
+    // pay the per-item hand-off: DESIGN.md §5), at least 8 pixels per lane.
     static const int target_blocks = [] {
         const char* e = getenv("YOUTH_ICP_TARGET_CHUNKS");  // tuning knob
         const int v = e ? atoi(e) : 0;
-        return v > 0 ? v : 2048;
+        return v > 0 ? v : 3072;
     }();
     int nb = (target_blocks + n_pairs - 1) / n_pairs;
     const int max_nb = (c->N + 2 * kRedStep - 1) / (2 * kRedStep);
@@ -1086,7 +1163,7 @@ static int launch_reduce(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, P
         if (rc) return rc;
     }
     const float thr2 = c->prm.dist_thresh * c->prm.dist_thresh;
-    const bool aligned = (reinterpret_cast<uintptr_t>(dsrc) % 8 == 0) && (c->N % 4 == 0);
+    const bool aligned = (reinterpret_cast<uintptr_t>(dsrc) % 8 == 0) && (c->W % 4 == 0);
     dim3 grid(nb, n_pairs);
     EventPair ep{};
     rc = ev_begin(c, s, &ep, 0);
@@ -1137,14 +1214,14 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
         const int nb = reduce_geometry(c, n_pairs, &chunk);
         rc = ensure_partials(c, (size_t)nb * n_pairs * kNeq);
         if (rc) return rc;
-        const bool aligned = (reinterpret_cast<uintptr_t>(dsrc) % 8 == 0) && (c->N % 4 == 0);
+        const bool aligned = (reinterpret_cast<uintptr_t>(dsrc) % 8 == 0) && (c->W % 4 == 0);
         const int var = (c->fast ? 2 : 0) | (aligned ? 1 : 0);
         const long long items = (long long)iters * n_pairs * nb;
         long long grid = (long long)c->n_cu * c->icp_blocks_per_cu[var];
         if (grid > items) grid = items;
         if (grid < 1) grid = 1;
         const IterState is{c->d_T64, c->d_T32, c->d_status, c->d_stats, c->d_arr_it, c->d_epoch,
-                           c->d_head, c->d_head + 1, iters, n_pairs, nb, chunk};
+                           c->d_head + kQHead, c->d_head + kQError, iters, n_pairs, nb, chunk};
         const float thr2 = c->prm.dist_thresh * c->prm.dist_thresh;
         EventPair ep{};
         rc = ev_begin(c, s, &ep, 0);
@@ -1174,7 +1251,7 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
 static int export_poses(youth_icp_ctx* c, hipStream_t s, int n_pairs, float* d_T_out)
 {
     hipLaunchKernelGGL(k_finish, dim3((n_pairs * 16 + 255) / 256), dim3(256), 0, s, c->d_T64,
-                       n_pairs, d_T_out, c->d_status, (const unsigned*)(c->d_head + 1));
+                       n_pairs, d_T_out, c->d_status, (const unsigned*)(c->d_head + kQError));
     HIP_TRY(hipGetLastError());
     return YOUTH_OK;
 }
@@ -1313,8 +1390,8 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
     if ((e = hipMalloc(&c->d_flag, 16)) != hipSuccess) return fail("hipMalloc flag", e);
     if ((e = hipMalloc(&c->d_epoch, MF * sizeof(unsigned))) != hipSuccess)
         return fail("hipMalloc epoch", e);
-    if ((e = hipMalloc(&c->d_head, 16)) != hipSuccess) return fail("hipMalloc head", e);
-    if ((e = hipMemset(c->d_head, 0, 16)) != hipSuccess) return fail("memset head", e);
+    if ((e = hipMalloc(&c->d_head, kQWords * 4)) != hipSuccess) return fail("hipMalloc head", e);
+    if ((e = hipMemset(c->d_head, 0, kQWords * 4)) != hipSuccess) return fail("memset head", e);
     {
         hipDeviceProp_t prop;
         if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess)
@@ -1442,6 +1519,19 @@ int youth_icp_set_timing(youth_icp_ctx* c, int enable)
         c->t_ms[k] = 0.0;
         c->t_n[k] = 0;
     }
+    return YOUTH_OK;
+}
+
+int youth_icp_get_sched_stats(youth_icp_ctx* c, unsigned* spins, unsigned* waited_items)
+{
+    if (!c) return set_error(YOUTH_EINVAL, "get_sched_stats: null context");
+    int rc = bind_device(c);
+    if (rc) return rc;
+    unsigned h[kQWords];
+    HIP_TRY(hipMemcpyAsync(h, c->d_head, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (spins) *spins = h[kQSpins];
+    if (waited_items) *waited_items = h[kQWaited];
     return YOUTH_OK;
 }
 

@@ -25,7 +25,7 @@ from ctypes import c_size_t, c_uint8, c_uint32, c_void_p
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libyouth_icp.so")
+LIB_PATH = os.environ.get("YOUTH_ICP_LIB") or os.path.join(HERE, "libyouth_icp.so")  # override: A/B builds (tools/ab.sh)
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "youth_icp.h")
 
 YOUTH_OK = 0
@@ -97,6 +97,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "youth_icp_get_stats": (c_int, [c_void_p, c_int, c_int, PD, PD]),
         "youth_icp_set_timing": (c_int, [c_void_p, c_int]),
         "youth_icp_get_timing": (c_int, [c_void_p, c_int, PD, POINTER(c_int)]),
+        "youth_icp_get_sched_stats": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_uint32)]),
         "youth_icp_prepare_host": (c_int, [c_void_p, P16, c_int, c_int, PF, PF, PF, PF, PF,
                                            PF]),
         "youth_icp_reduce_host": (c_int, [c_void_p, P16, P16, PF, PI32, PD]),
@@ -336,6 +337,13 @@ class IcpContext:
         _check(self._lib.youth_icp_get_timing(self._ctx, kind, ctypes.byref(ms),
                                               ctypes.byref(n)))
         return ms.value, n.value
+
+    def get_sched_stats(self):
+        """(epoch polls, items that waited) of the last persistent align."""
+        spins, waited = c_uint32(0), c_uint32(0)
+        _check(self._lib.youth_icp_get_sched_stats(self._ctx, ctypes.byref(spins),
+                                                   ctypes.byref(waited)))
+        return spins.value, waited.value
 
     # host-array stage entry points (parity tests)
     def prepare(self, depth: np.ndarray, want_normals: bool = True):

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Build libyouth_icp.so from a git revision of csrc/icp_kernels.hip into
+# tools/ab/<name>/ so two kernel versions can be timed in ONE gpurun call
+# (devices differ by several % on this VALU-bound kernel; never compare
+# across boxes).  Usage: tools/ab_build.sh <name> <git-rev | file.hip>
+set -euo pipefail
+NAME=$1; SRC=$2
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+OUT=$ROOT/tools/ab/$NAME
+mkdir -p $OUT
+if [ -f "$SRC" ]; then cp "$SRC" $OUT/icp_kernels.hip
+else git -C $ROOT show "$SRC:slam-rgbd_amd/csrc/icp_kernels.hip" > $OUT/icp_kernels.hip; fi
+cd $ROOT/slam-rgbd_amd
+make -s build/slam_api.o build/algorithm_module.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
+    -I../include -Icsrc -c $OUT/icp_kernels.hip -o $OUT/icp_kernels.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libyouth_icp.so $OUT/icp_kernels.o \
+    build/slam_api.o build/algorithm_module.o -lpthread -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
+echo "$OUT/libyouth_icp.so"

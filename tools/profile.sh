@@ -6,7 +6,7 @@
 # Usage: tools/profile.sh <tag> [bench args...]
 set -euo pipefail
 TAG=${1:-r01}; shift || true
-ARGS=${*:---steps 10 --warmup 2 --no-cpu-baseline}
+ARGS=${*:---steps 30 --warmup 5 --no-cpu-baseline}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
@@ -16,6 +16,6 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -T --output-format c
     -- python3 bench.py $ARGS > $OUT/bench_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -T --output-format csv -d $OUT/pmc_write -o pmc \
     -- python3 bench.py $ARGS > $OUT/bench_write.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD --kernel-trace -T --output-format csv -d $OUT/pmc_sq -o pmc \
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE --kernel-trace -T --output-format csv -d $OUT/pmc_sq -o pmc \
     -- python3 bench.py $ARGS > $OUT/bench_sq.log 2>&1
 echo done
