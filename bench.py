@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpus)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-io", action="store_true",
+                    help="skip the PCIe-inclusive host-buffer API leg (rank 0, N=1)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per k_reduce launch (tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -107,7 +109,7 @@ class Run:
         pixels_per_launch = pixels_per_iter * iters_per_launch
         alg = BYTES_PER_PX_ITER * pixels_per_launch
         own = KERNEL_BYTES_PER_PX * pixels_per_launch
-        traffic, src = None, None
+        traffic, src, valu = None, None, None
         if os.path.exists(self.a.traffic_json):
             try:
                 tj = json.load(open(self.a.traffic_json))
@@ -116,6 +118,10 @@ class Run:
                     per_iter = tj.get("hbm_bytes_per_iteration", tj.get("hbm_bytes_per_launch"))
                     traffic = per_iter * iters_per_launch
                     src = os.path.relpath(self.a.traffic_json, ROOT)
+                    if "valu_issue_frac" in tj:   # PMC SQ pass of the same kernel
+                        valu = {k: tj[k] for k in ("valu_issue_frac",
+                                                   "valu_lane_ops_per_px_iteration",
+                                                   "effective_clock_ghz") if k in tj}
             except (OSError, ValueError, TypeError):
                 traffic = None
         achieved = alg / (avg * 1e-3) / 1e9
@@ -123,6 +129,7 @@ class Run:
             "bound": "hbm",
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
+            "valu_limit": valu,
             "algorithmic_bytes_per_launch": alg,
             "algorithmic_model": "SURVEY §8d: 36 B/px/iter x pixels x pairs",
             "kernel_bytes_per_launch": own,
@@ -168,6 +175,8 @@ def run_pairs(R):
     result["kernel_ms_per_step"] = {k: v[0] / a.steps for k, v in kt.items()}
     spins, waited = ctx.get_sched_stats()   # last align: persistent-kernel pose waits
     result["sched_last_step"] = {"epoch_polls": spins, "items_waited": waited}
+    if rank == 0 and world == 1 and not a.no_host_io:
+        result["host_io"] = host_io_rate(a, src, dst)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         result["cpu_baseline"], result["parity"] = cpu_baseline(a, src, dst, T_gpu)
     ctx.close()
@@ -230,6 +239,24 @@ def base_result(R, value, elapsed):
         "data": "synthetic (ray-cast room scene, int16 mm depth, seeds 0x5EED0000+pair / "
                 "0x5EED1000 sequence)",
     }
+
+
+def host_io_rate(a, src, dst, reps=5):
+    """PCIe-inclusive rate of the one-shot host API (youth_icp_align_batch):
+    H2D of both depth stacks + align + D2H of the poses, synchronous, from
+    pageable (numpy) and pinned (torch pin_memory) host buffers.  Reported
+    beside the bench value, never as it (inputs there are resident in HBM)."""
+    out = {"api": "youth_icp_align_batch", "pairs": int(src.shape[0]),
+           "h2d_bytes_per_pair": int(2 * src[0].nbytes)}
+    ps = torch.from_numpy(src).pin_memory()
+    pd = torch.from_numpy(dst).pin_memory()
+    for kind, (s, d) in (("pageable", (src, dst)), ("pinned", (ps.numpy(), pd.numpy()))):
+        youth_icp.align_batch(s, d, iters=a.iters)          # warm: batch context, pages
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            youth_icp.align_batch(s, d, iters=a.iters)
+        out[kind + "_aligns_per_s"] = reps * src.shape[0] / (time.perf_counter() - t0)
+    return out
 
 
 def cpu_baseline(a, src, dst, T_gpu):

@@ -7,7 +7,7 @@ mkdir -p gpurun_out/ab
 for r in $(seq 1 $R); do
   for n in "$@"; do
     YOUTH_ICP_LIB=tools/ab/$n/libyouth_icp.so timeout -k 10 240 python3 bench.py --steps 30 --warmup 5 \
-        --no-cpu-baseline ${EXTRA:-} > gpurun_out/ab/$n.$r.json 2> gpurun_out/ab/$n.$r.err
+        --no-cpu-baseline --no-host-io ${EXTRA:-} > gpurun_out/ab/$n.$r.json 2> gpurun_out/ab/$n.$r.err
     python3 - "$n" "$r" <<'PY'
 import json,sys
 d=json.loads(open(f"gpurun_out/ab/{sys.argv[1]}.{sys.argv[2]}.json").read().strip().splitlines()[-1])

@@ -7,12 +7,23 @@ gfx950 correction, re-calibrated here: tools/kbench's k_stream_read of a known
 550.5 MB reports FETCH_SIZE = 275.3 MB for both dwordx4 and dword loads
 (profiles/r01/pmc_calibration.txt).
 
+VALU issue: when the SQ pass holds SQ_INSTS_VALU and GRBM_GUI_ACTIVE, also
+  effective clock = GRBM_GUI_ACTIVE / n_XCD / kernel duration (MI355X_MICROARCH.md
+                    "DVFS give-back": rocprofv3 sums GRBM over the 8 XCDs),
+  VALU issue fraction = SQ_INSTS_VALU x 4 cycles / (SIMDs x GRBM_GUI_ACTIVE / n_XCD)
+(a wave64 VALU instruction occupies its SIMD16 for 4 cycles; fp64 FMA is
+full rate on gfx950).  SIMD count from the pass's agent_info.csv.
+
 usage: tools/pmc_traffic.py <profile_root> <out.json> <pairs> <width> <height> [iters]
 (iters: ICP iterations each k_icp launch covers; 1 for per-iteration k_reduce)
 """
+import csv
+import glob
 import json
 import os
 import sys
+
+N_XCD = 8
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_summary import summarize  # noqa: E402
@@ -37,6 +48,28 @@ def main():
         "bytes_per_px": (2.0 * fetch + write) / iters / px,
         "correction": "2 x FETCH_SIZE (gfx950 tallies 128-B requests as 64 B)",
     }
+    if "SQ_INSTS_VALU" in r and "GRBM_GUI_ACTIVE" in r:
+        simds = 1024
+        for f in glob.glob(os.path.join(root, "*", "*agent_info.csv")):
+            for a in csv.DictReader(open(f)):
+                if a.get("Name", "").startswith("gfx") and a.get("Simd_Count"):
+                    simds = int(a["Simd_Count"])
+        cyc = r["GRBM_GUI_ACTIVE"] / N_XCD
+        doc["valu_wave_instructions_per_launch"] = r["SQ_INSTS_VALU"]
+        doc["valu_lane_ops_per_px_iteration"] = r["SQ_INSTS_VALU"] * 64 / (px * iters)
+        doc["valu_issue_frac"] = r["SQ_INSTS_VALU"] * 4.0 / (simds * cyc)
+        doc["gpu_cycles_per_launch"] = cyc
+        doc["simds"] = simds
+        durs = []
+        for f in glob.glob(os.path.join(root, "*", "*kernel_trace.csv")):
+            if "sq" not in os.path.basename(os.path.dirname(f)):
+                continue
+            for row in csv.DictReader(open(f)):
+                if key in row.get("Kernel_Name", ""):
+                    durs.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+        if durs:
+            avg_ns = sum(durs) / len(durs)
+            doc["effective_clock_ghz"] = cyc / avg_ns
     for k in ("k_prep", "k_solve"):
         m = next((x for x in res if x.startswith(k)), None)
         if m and "FETCH_SIZE" in res[m]:
