@@ -193,6 +193,14 @@ int youth_icp_get_timing(youth_icp_ctx* ctx, int kind, double* total_ms,
 int youth_icp_get_sched_stats(youth_icp_ctx* ctx, unsigned* spins,
                               unsigned* waited_items);
 
+/* Validation: compare the kernels' shared-reciprocal projection division with
+ * IEEE fp32 a/b on n pseudo-random cases (seeded) on `device`.
+ * *bit_mismatches counts bitwise differences where the IEEE expansion does not
+ * rescale (must be 0); *proj_mismatches counts differences of the projected
+ * pixel floor((q + c) + 0.5) or its in-range test over all cases (must be 0). */
+int youth_icp_selftest_projdiv(int device, long long n, unsigned long long seed,
+                               long long* bit_mismatches, long long* proj_mismatches);
+
 /* --- Stage-level entry points (validation / parity tests) --------------- */
 
 /* Depth -> XYZ planes (+ normals when want_normals) for n_frames host frames.

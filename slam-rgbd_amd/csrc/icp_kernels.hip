@@ -86,6 +86,36 @@ __device__ __forceinline__ float bp_div(float n, float d, float rd)
     return kFast ? div_fast(n, d, rd) : n / d;
 }
 
+// Spec a7's two projection quotients nu/den and nv/den, IEEE correctly
+// rounded, sharing one reciprocal.  hipcc expands an fp32 a/b (denormals on)
+// to  s = div_scale(b,b,a); n = div_scale(a,b,a); r = rcp(s);
+//     r = fma(fma(-s,r,1), r, r); q = n*r; q = fma(fma(-s,q,n), r, q);
+//     q = div_fmas(fma(-s,q,n), r, q); result = div_fixup(q, b, a)   (`make asm`).
+// For b in [2^-60, 2^60] div_scale rescales neither operand except when a is
+// 0, |a/b| >= ~2^95, |a/b| < 2^-126 or |a| < 2^-103; otherwise div_fmas is a
+// plain fma and div_fixup returns q unchanged, so the chain below equals a/b
+// bit for bit, and its reciprocal part depends on b only.  In the excepted
+// cases the results differ at most between 0 / tiny / huge / inf / NaN
+// values, which the projection (+cx, +0.5, floor, range test) maps to the same
+// pixel or to "outside".  Callers fall back to a/b when b is out of range.
+// youth_icp_selftest_projdiv compares the two bitwise on random and edge
+// cases (tests/test_gpu_parity.py).
+__device__ __forceinline__ float proj_div_one(float n, float den, float r)
+{
+    float q = n * r;
+    q = fmaf(fmaf(-den, q, n), r, q);
+    return fmaf(fmaf(-den, q, n), r, q);
+}
+__device__ __forceinline__ float proj_recip(float den)
+{
+    const float r0 = __builtin_amdgcn_rcpf(den);
+    return fmaf(fmaf(-den, r0, 1.0f), r0, r0);
+}
+__device__ __forceinline__ bool proj_den_ok(float den)
+{
+    return (den >= 0x1p-60f) & (den <= 0x1p60f);
+}
+
 // viewerModule.c:341-345 with explicit intrinsics (bit-identical to the
 // viewer for cx = W/2, cy = H/2, f = 570.3f, ds = 1000.0f):
 //   valid iff d > 0;  z = d / ds;  x = ((u - cx) z) / fx;  y = ((v - cy) z) / fy
@@ -118,6 +148,75 @@ __global__ void k_verify_fastdiv(Intr K, FastK F, int W, int H, unsigned* bad)
         nb += (div_fast(n, K.fy, F.rfy) != n / K.fy);
     }
     if (nb) atomicAdd(bad, nb);
+}
+
+// Bitwise self-test of the shared-reciprocal projection division
+// (proj_recip / proj_div_one) against IEEE a/b on `n` SplitMix64 cases:
+//   mode 0: random den in [2^-60, 2^60], num with exponent in [-80, 80];
+//   mode 1: quotients next to half-integers (the rounding-critical case of
+//           floor(q + c + 0.5)): num = RN(den * (m + 0.5)) +- a few ulps;
+//   mode 2: den in range, num any finite fp32 bit pattern (incl. 0, tiny,
+//           denormal, huge);
+//   mode 3: den near the guard bounds 2^+-60, num random.
+// bad[0]: bit mismatches where div_scale does not rescale (must be 0);
+// bad[1]: mismatches of the projection outcome floor((q + c) + 0.5) and its
+//         in-range test [0, 65536) for c in [0, 4096) (must be 0), all cases.
+__device__ __forceinline__ unsigned long long sm64(unsigned long long& x)
+{
+    unsigned long long z = (x += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__global__ void k_selftest_projdiv(unsigned long long n, unsigned long long seed,
+                                   unsigned long long* bad)
+{
+    unsigned long long b0 = 0, b1 = 0;
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += stride) {
+        unsigned long long st = seed ^ (i * 0xD1B54A32D192ED03ull);
+        const unsigned long long r1 = sm64(st), r2 = sm64(st), r3 = sm64(st);
+        const int mode = (int)(i & 3);
+        float den;
+        if (mode == 3) {
+            const int e = (r1 & 1) ? 60 : -60;
+            den = __uint_as_float((unsigned)((e + 127) << 23) | (unsigned)(r2 & 0x7FFFFF));
+            if (r1 & 2) den = __uint_as_float(__float_as_uint(den) - (unsigned)((r3 >> 40) & 0xFF));
+        } else {
+            const int e = (int)(r1 % 121) - 60;
+            den = __uint_as_float((unsigned)((e + 127) << 23) | (unsigned)(r2 & 0x7FFFFF));
+        }
+        float num;
+        if (mode == 1) {
+            const float m = (float)((int)(r3 % 8192) - 4096) + 0.5f;
+            num = den * m;
+            num = __uint_as_float(__float_as_uint(num) + (unsigned)((int)((r3 >> 20) & 7) - 3));
+        } else if (mode == 2) {
+            unsigned bits = (unsigned)(r3 >> 8);
+            if (((bits >> 23) & 0xFF) == 0xFF) bits &= ~(1u << 30);  // finite only
+            num = __uint_as_float(bits);
+        } else {
+            const int e = (int)((r3 >> 8) % 161) - 80;
+            num = __uint_as_float((unsigned)((e + 127) << 23) | (unsigned)(r3 & 0x7FFFFF) |
+                                  (unsigned)((r3 >> 63) << 31));
+        }
+        if (!proj_den_ok(den)) continue;
+        const float q_ieee = num / den;
+        const float q_fast = proj_div_one(num, den, proj_recip(den));
+        const float aq = fabsf(q_ieee), an = fabsf(num);
+        const int en = (int)((__float_as_uint(num) >> 23) & 0xFF);
+        const int ed = (int)((__float_as_uint(den) >> 23) & 0xFF);
+        const bool noscale = num != 0.0f && en - ed < 96 && en > 23 && aq >= 0x1p-126f &&
+                             an == an;
+        if (noscale && __float_as_uint(q_ieee) != __float_as_uint(q_fast)) ++b0;
+        const float c = (float)(r2 >> 52);  // [0, 4096)
+        const float ui = floorf((q_ieee + c) + 0.5f), uf = floorf((q_fast + c) + 0.5f);
+        const bool ii = (ui >= 0.0f) & (ui < 65536.0f), inf_ = (uf >= 0.0f) & (uf < 65536.0f);
+        if (ii != inf_ || (ii && ui != uf)) ++b1;
+    }
+    if (b0) atomicAdd(bad + 0, b0);
+    if (b1) atomicAdd(bad + 1, b1);
 }
 
 // ------------------------------------------------------------------ k_prep --
@@ -511,8 +610,18 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
             qz[q] = ((T[8] * sx + T[9] * sy) + T[10] * sz) + T[11];
             const bool vz = (sz > 0.0f) & (qz[q] > 0.0f);
             const float qzs = vz ? qz[q] : 1.0f;
-            const float uu = floorf((((K.fx * qx[q]) / qzs) + K.cx) + 0.5f);
-            const float vv = floorf((((K.fy * qy[q]) / qzs) + K.cy) + 0.5f);
+            const float nu = K.fx * qx[q], nv = K.fy * qy[q];
+            float du, dv;
+            if (proj_den_ok(qzs)) {  // always in practice (qz is a depth in metres)
+                const float r = proj_recip(qzs);
+                du = proj_div_one(nu, qzs, r);
+                dv = proj_div_one(nv, qzs, r);
+            } else {
+                du = nu / qzs;
+                dv = nv / qzs;
+            }
+            const float uu = floorf((du + K.cx) + 0.5f);
+            const float vv = floorf((dv + K.cy) + 0.5f);
             in[q] = vz & (uu >= 0.0f) & (uu < (float)W) & (vv >= 0.0f) & (vv < (float)H);
             fu[q] = in[q] ? uu : 0.0f;
             fv[q] = in[q] ? vv : 0.0f;
@@ -1519,6 +1628,31 @@ int youth_icp_set_timing(youth_icp_ctx* c, int enable)
         c->t_ms[k] = 0.0;
         c->t_n[k] = 0;
     }
+    return YOUTH_OK;
+}
+
+int youth_icp_selftest_projdiv(int device, long long n, unsigned long long seed,
+                               long long* bit_mismatches, long long* proj_mismatches)
+{
+    if (n < 0) return set_error(YOUTH_EINVAL, "selftest_projdiv: n < 0");
+    const int ndev = youth_icp_device_count();
+    if (ndev <= 0 || device < 0 || device >= ndev)
+        return set_error(YOUTH_ENODEV, "selftest_projdiv: no HIP device %d", device);
+    HIP_TRY(hipSetDevice(device));
+    unsigned long long* d_bad = nullptr;
+    HIP_TRY(hipMalloc(&d_bad, 2 * sizeof(unsigned long long)));
+    unsigned long long h[2] = {0, 0};
+    hipError_t e = hipMemset(d_bad, 0, sizeof(h));
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_selftest_projdiv, dim3(4096), dim3(256), 0, 0,
+                           (unsigned long long)n, seed, d_bad);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(h, d_bad, sizeof(h), hipMemcpyDeviceToHost);
+    (void)hipFree(d_bad);
+    if (e != hipSuccess) return set_error(YOUTH_EHIP, "selftest_projdiv: %s", hipGetErrorString(e));
+    if (bit_mismatches) *bit_mismatches = (long long)h[0];
+    if (proj_mismatches) *proj_mismatches = (long long)h[1];
     return YOUTH_OK;
 }
 

@@ -98,6 +98,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "youth_icp_set_timing": (c_int, [c_void_p, c_int]),
         "youth_icp_get_timing": (c_int, [c_void_p, c_int, PD, POINTER(c_int)]),
         "youth_icp_get_sched_stats": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_uint32)]),
+        "youth_icp_selftest_projdiv": (c_int, [c_int, ctypes.c_longlong, ctypes.c_ulonglong,
+                                               POINTER(ctypes.c_longlong),
+                                               POINTER(ctypes.c_longlong)]),
         "youth_icp_prepare_host": (c_int, [c_void_p, P16, c_int, c_int, PF, PF, PF, PF, PF,
                                            PF]),
         "youth_icp_reduce_host": (c_int, [c_void_p, P16, P16, PF, PI32, PD]),
@@ -118,8 +121,14 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "youth_slam_wait_idle": (c_int, [c_int]),
         "youth_slam_wait_stopped": (None, []),
     }
+    ab_build = bool(os.environ.get("YOUTH_ICP_LIB"))  # tools/ab_*.sh: older builds
     for name, (res, args) in sig.items():
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            if ab_build:
+                continue
+            raise
         fn.restype = res
         fn.argtypes = args
     _lib = lib
@@ -384,6 +393,15 @@ class IcpContext:
 
     def track_reset(self) -> None:
         self._lib.youth_icp_track_reset(self._ctx)
+
+
+def selftest_projdiv(n: int, seed: int = 1, device: int = 0) -> tuple[int, int]:
+    """youth_icp_selftest_projdiv: (bit mismatches, projection mismatches) of the
+    kernels' shared-reciprocal projection division vs IEEE a/b on n cases."""
+    lib = load_library()
+    b, p = ctypes.c_longlong(0), ctypes.c_longlong(0)
+    _check(lib.youth_icp_selftest_projdiv(device, n, seed, ctypes.byref(b), ctypes.byref(p)))
+    return b.value, p.value
 
 
 def align_batch(src: np.ndarray, dst: np.ndarray, K: Intrinsics | None = None, iters: int = 10,

@@ -304,6 +304,16 @@ def test_algorithm_module_thread_entry():
 
 
 # ------------------------------------------------ division path / alignment --
+def test_projection_division_matches_ieee():
+    """The shared-reciprocal projection divide (icp_kernels.hip proj_div_one)
+    equals IEEE a/b bit for bit wherever the IEEE expansion does not rescale,
+    and gives the same projected pixel / in-range decision everywhere:
+    2 x 2^30 random, near-half-integer, arbitrary-bit and guard-edge cases."""
+    for seed in (1, 0x5EED):
+        bits, proj = youth_icp.selftest_projdiv(1 << 30, seed)
+        assert bits == 0 and proj == 0, (seed, bits, proj)
+
+
 def test_fastdiv_path_is_bit_identical_to_ieee(monkeypatch):
     """The verified 3-op back-projection divide must change nothing: both
     paths give the same association and bit-identical poses."""

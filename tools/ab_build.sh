@@ -3,6 +3,7 @@
 # tools/ab/<name>/ so two kernel versions can be timed in ONE gpurun call
 # (devices differ by several % on this VALU-bound kernel; never compare
 # across boxes).  Usage: tools/ab_build.sh <name> <git-rev | file.hip>
+# (env HIPFLAGS_EXTRA: extra hipcc flags for the kernel TU; product flags are the Makefile's)
 set -euo pipefail
 NAME=$1; SRC=$2
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -12,8 +13,8 @@ if [ -f "$SRC" ]; then cp "$SRC" $OUT/icp_kernels.hip
 else git -C $ROOT show "$SRC:slam-rgbd_amd/csrc/icp_kernels.hip" > $OUT/icp_kernels.hip; fi
 cd $ROOT/slam-rgbd_amd
 make -s build/slam_api.o build/algorithm_module.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math \
-    -I../include -Icsrc -c $OUT/icp_kernels.hip -o $OUT/icp_kernels.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize \
+    ${HIPFLAGS_EXTRA:-} -I../include -Icsrc -c $OUT/icp_kernels.hip -o $OUT/icp_kernels.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libyouth_icp.so $OUT/icp_kernels.o \
     build/slam_api.o build/algorithm_module.o -lpthread -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
 echo "$OUT/libyouth_icp.so"

@@ -112,6 +112,11 @@ int main(int argc, char** argv)
         {"prod fast aligned tb1024", 1024, 18, PROD(k_reduce<false, true, true, false>)},
         {"prod fast aligned tb8192", 8192, 18, PROD(k_reduce<false, true, true, false>)},
         {"prod ieee aligned tb2048", 2048, 18, PROD(k_reduce<false, false, true, false>)},
+        {"v5 packed pairs tb2048", 2048, 18, [=](dim3 g, int chunk, double* part) {
+             hipLaunchKernelGGL(k_reduce_v5<true>, g, dim3(kRedThreads), 0, st,
+                                (const int16_t*)d_src, (const float4*)rec, Pp, pm_prod, W, H, Ki,
+                                Fk, thr2, chunk, part, T32);
+         }},
         {"pf depth-prefetch tb2048", 2048, 18, [=](dim3 g, int chunk, double* part) {
              hipLaunchKernelGGL((k_reduce_pf<true, true>), g, dim3(kRedThreads), 0, st,
                                 (const int16_t*)d_src, (const float4*)rec, Pp, pm_prod, W, H, Ki,
@@ -153,6 +158,7 @@ int main(int argc, char** argv)
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     std::vector<std::vector<double>> sums(vs.size());
+    std::vector<std::vector<double>> parts(vs.size());  // raw partials of round 0
     std::vector<std::vector<float>> times(vs.size());
     const int rounds = 5;
     for (int r = 0; r < rounds; ++r) {
@@ -172,6 +178,7 @@ int main(int argc, char** argv)
             if (r == 0) {
                 std::vector<double> part((size_t)n * nb * kNeq);
                 CK(hipMemcpy(part.data(), d_part, part.size() * 8, hipMemcpyDeviceToHost));
+                parts[v] = part;
                 sums[v].assign((size_t)n * kNeq, 0.0);
                 for (int p = 0; p < n; ++p)
                     for (int b = 0; b < nb; ++b)
@@ -181,8 +188,13 @@ int main(int argc, char** argv)
         }
     }
     const double px = (double)N * n;
-    printf("%-28s %9s %9s %10s %11s %12s\n", "variant", "med_us", "min_us", "GB/s@36B",
-           "GB/s(own)", "max_rel_diff");
+    // bitwise check of every partial word against the production kernel at
+    // the same geometry (same summation tree => must be identical)
+    int ref = -1;
+    for (size_t v = 0; v < vs.size(); ++v)
+        if (strncmp(vs[v].name, "prod fast aligned", 17) == 0 && ref < 0) ref = (int)v;
+    printf("%-28s %9s %9s %10s %11s %12s %10s\n", "variant", "med_us", "min_us", "GB/s@36B",
+           "GB/s(own)", "max_rel_diff", "bits!=prod");
     for (size_t v = 0; v < vs.size(); ++v) {
         auto t = times[v];
         std::sort(t.begin(), t.end());
@@ -192,8 +204,14 @@ int main(int argc, char** argv)
             if (std::fabs(b) > 1e-6) md = std::max(md, std::fabs(a - b) / std::fabs(b));
         }
         const double med = t[t.size() / 2] * 1e-6;
-        printf("%-28s %9.1f %9.1f %10.0f %11.0f %12.3e\n", vs[v].name, t[t.size() / 2], t[0],
-               36.0 * px / med / 1e9, vs[v].bpp * px / med / 1e9, md);
+        long nbits = -1;
+        if (ref >= 0 && vs[v].tb == vs[ref].tb && parts[v].size() == parts[ref].size()) {
+            nbits = 0;
+            for (size_t k = 0; k < parts[v].size(); ++k)
+                nbits += memcmp(&parts[v][k], &parts[ref][k], 8) != 0;
+        }
+        printf("%-28s %9.1f %9.1f %10.0f %11.0f %12.3e %10ld\n", vs[v].name, t[t.size() / 2],
+               t[0], 36.0 * px / med / 1e9, vs[v].bpp * px / med / 1e9, md, nbits);
     }
     youth_icp_destroy(c);
     return 0;
