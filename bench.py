@@ -260,27 +260,43 @@ def host_io_rate(a, src, dst, reps=5):
 
 
 def cpu_baseline(a, src, dst, T_gpu):
-    """The C oracle on host cores over a bounded sample of the same pairs
-    (OpenMP over pairs); also the SE(3) error of the GPU poses on it."""
+    """The C oracle on the host cores of the GPU box over a bounded sample of
+    the same pairs: one warm-up, then the median of >= 5 timed
+    passes, (i) OpenMP over pairs on up to 16 threads (the reported value),
+    (ii) one thread on a 2-pair sample; also the SE(3) error of the GPU poses."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
 
     cpus = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     threads = a.cpu_threads or min(16, cpus or 1)
     S = src.shape[0]
-    oracle.align_batch(src[:1], dst[:1], iters=a.iters, n_threads=1)  # warm
-    # repeat passes over the rank-0 pairs until ~1.5 s wall (~10-30 s of CPU work)
-    passes, wall, T_cpu, st = 0, 0.0, None, None
-    while wall < 1.5 and passes < 50:
+    oracle.align_batch(src[:threads], dst[:threads], iters=a.iters, n_threads=threads)  # warm
+    rates, T_cpu, st = [], None, None
+    while len(rates) < 5 or (sum(S / r for r in rates) < 1.5 and len(rates) < 50):
         t0 = time.perf_counter()
         T_cpu, st = oracle.align_batch(src, dst, iters=a.iters, n_threads=threads)
-        wall += time.perf_counter() - t0
-        passes += 1
+        rates.append(S / (time.perf_counter() - t0))
+    single = []
+    oracle.align_batch(src[:1], dst[:1], iters=a.iters, n_threads=1)  # warm
+    for _ in range(5):
+        t0 = time.perf_counter()
+        oracle.align_batch(src[:2], dst[:2], iters=a.iters, n_threads=1)
+        single.append(2 / (time.perf_counter() - t0))
     err = float(np.abs(T_gpu[:, :3, :] - T_cpu[:, :3, :]).max())
-    cpu = {"value": passes * S / wall, "unit": "aligns/s", "cores": threads, "kind": "port",
-           "sample": f"{passes} pass(es) over the {S} rank-0 pairs ({a.width}x{a.height}, "
-                     f"{a.iters} iters): C oracle -O3 -ffp-contract=off, OpenMP over pairs, "
-                     f"{wall:.2f} s wall"}
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")),
+                         "")
+    except OSError:
+        pass
+    cpu = {"value": float(np.median(rates)), "unit": "aligns/s", "cores": threads, "kind": "port",
+           "sample": f"median of {len(rates)} passes over the {S} rank-0 pairs ({a.width}x"
+                     f"{a.height}, {a.iters} iters) after 1 warm-up: C oracle -O3 "
+                     f"-ffp-contract=off, OpenMP over pairs",
+           "single_thread": {"value": float(np.median(single)), "unit": "aligns/s", "cores": 1,
+                             "sample": "median of 5 passes over 2 pairs"},
+           "host": {"cpu_model": model, "cpus_visible": cpus}}
     parity = {"pose_max_abs_err_vs_cpu": err, "pairs_checked": S, "tolerance": 1e-5,
               "cpu_status_nonzero": int((st != 0).sum())}
     return cpu, parity
