@@ -269,6 +269,9 @@ int youth_slam_trajectory_length(void);
 /* Copy up to n trajectory entries: timestamps [n] and world poses [n][16]
  * (fp64 row-major, first frame = identity).  Returns the count copied. */
 int youth_slam_get_trajectory(int n, uint32_t* timestamps, double* T_wc);
+/* Entry `index` of the trajectory: 1 with *timestamp / T_wc[16] filled, 0 if
+ * index is out of range. */
+int youth_slam_get_pose(int index, uint32_t* timestamp, double* T_wc);
 /* Block until the ingest queue is empty and the worker is idle, or
  * timeout_ms elapses.  Returns 1 when drained, 0 on timeout / not running. */
 int youth_slam_wait_idle(int timeout_ms);

@@ -462,6 +462,15 @@ int youth_slam_get_trajectory(int n, uint32_t* timestamps, double* T_wc)
     return m;
 }
 
+int youth_slam_get_pose(int index, uint32_t* timestamp, double* T_wc)
+{
+    std::lock_guard<std::mutex> lk(g_slam_mu);
+    if (index < 0 || index >= (int)g_traj.size()) return 0;
+    if (timestamp) *timestamp = g_traj[index].ts;
+    if (T_wc) memcpy(T_wc, g_traj[index].T, sizeof(g_traj[index].T));
+    return 1;
+}
+
 int youth_slam_wait_idle(int timeout_ms)
 {
     const auto t0 = std::chrono::steady_clock::now();

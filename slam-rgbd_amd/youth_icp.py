@@ -136,11 +136,15 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
 
 
 def declared_functions(header: str = HEADER_PATH) -> list[str]:
-    """Function names declared in include/youth_icp.h (for the ABI test)."""
+    """Function names declared in an include/*.h header (for the ABI test);
+    function-pointer typedefs and keywords are not functions."""
     text = open(header).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = re.sub(r"typedef[^;]*;", "", text)
     names = re.findall(r"\b([A-Za-z_]\w*)\s*\([^;{]*\)\s*;", text)
-    return sorted({n for n in names if n not in ("sizeof",)})
+    keywords = {"sizeof", "int", "void", "char", "unsigned", "double", "float", "long", "short",
+                "const", "return", "if", "while", "for", "struct"}
+    return sorted({n for n in names if n not in keywords})
 
 
 def _p(arr, ctype):

@@ -86,7 +86,29 @@ def make_seq_case(name, W, H, n_frames, iters=10, dist=0.10):
     print(f"{name}: {n_frames} frames")
 
 
+def make_recording(name, n=3, W=24, H=16, seed=7):
+    """A .bin recording written with Python's struct module from the
+    reference's layouts (FrameHeader '<IIHHH2xIII', frameDefinitions.h:11-20;
+    frame = header + int16 depth + uint8 RGB, loggingModule.c:101-130; end
+    marker = zero header with frameType 0xFF, :224-226) — independent of the
+    C writer it is used to check (tests/test_wire.py)."""
+    import struct
+    fh = struct.Struct("<IIHHH2xIII")
+    rng = np.random.default_rng(seed)
+    b = bytearray()
+    for k in range(n):
+        d = rng.integers(-5, 9000, (H, W)).astype(np.int16)
+        c = rng.integers(0, 256, (H, W, 3)).astype(np.uint8)
+        b += fh.pack(100 + k, 1000 + 33 * k, 1, W, H, W * H * 2, W * H * 3, 0)
+        b += d.astype("<i2").tobytes() + c.tobytes()
+    b += fh.pack(0, 0, 0xFF, 0, 0, 0, 0, 0)
+    with open(os.path.join(HERE, name), "wb") as f:
+        f.write(bytes(b))
+    print(f"{name}: {n} frames, {len(b)} bytes")
+
+
 def main():
+    make_recording("rec_24x16_3f.bin")
     np.savez_compressed(os.path.join(HERE, "kat_backproject.npz"),
                         table=np.array(KAT, dtype=np.int64))
     make_pair_case("pair_80x60", 80, 60, 0)

@@ -15,6 +15,7 @@ from conftest import GOLDEN, PKG, ROOT
 
 HEADERS = {
     "youth_icp.h": os.path.join(PKG, "libyouth_icp.so"),
+    "youth_wire.h": os.path.join(PKG, "libyouth_icp.so"),
     "youth_synth.h": os.path.join(PKG, "libyouth_synth.so"),
 }
 
@@ -45,7 +46,8 @@ def test_reference_api_names_present():
 
 
 def test_header_compiles_as_c99_and_cpp():
-    src = '#include "youth_icp.h"\n#include "youth_synth.h"\nint main(void){return 0;}\n'
+    src = ('#include "youth_icp.h"\n#include "youth_synth.h"\n#include "youth_wire.h"\n'
+           'int main(void){return 0;}\n')
     inc = os.path.join(ROOT, "include")
     for cc, std in (("gcc", "-std=c99"), ("g++", "-std=c++11")):
         r = subprocess.run([cc, std, "-Wall", "-Werror", "-fsyntax-only", "-I", inc, "-x",

@@ -283,8 +283,12 @@ def test_slam_api_end_to_end():
     assert youth_icp.processSlamFrame(frames[0], None, 640, 480, 0) == 0
 
 
-def test_algorithm_module_thread_entry():
+def test_algorithm_module_thread_entry(monkeypatch):
     import threading
+    import youth_wire
+    fq = f"/youth_t_entry_{os.getpid()}"
+    monkeypatch.setenv("YOUTH_ALGO_FRAME_QUEUE", fq)      # private queue, no pose queue
+    monkeypatch.setenv("YOUTH_ALGO_POSE_QUEUE", "")
     lib = youth_icp.load_library()
     t = threading.Thread(target=lambda: lib.algorithmModule(None))
     t.start()
@@ -301,6 +305,7 @@ def test_algorithm_module_thread_entry():
     youth_icp.stopSlamModule()
     t.join(timeout=10)
     assert not t.is_alive()
+    youth_wire.mq_unlink(fq)
 
 
 # ------------------------------------------------ division path / alignment --
