@@ -12,9 +12,9 @@ mkdir -p $OUT
 if [ -f "$SRC" ]; then cp "$SRC" $OUT/icp_kernels.hip
 else git -C $ROOT show "$SRC:slam-rgbd_amd/csrc/icp_kernels.hip" > $OUT/icp_kernels.hip; fi
 cd $ROOT/slam-rgbd_amd
-make -s build/slam_api.o build/algorithm_module.o
+make -s build/slam_api.o build/algorithm_module.o build/wire.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize \
     ${HIPFLAGS_EXTRA:-} -I../include -Icsrc -c $OUT/icp_kernels.hip -o $OUT/icp_kernels.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libyouth_icp.so $OUT/icp_kernels.o \
-    build/slam_api.o build/algorithm_module.o -lpthread -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
+    build/slam_api.o build/algorithm_module.o build/wire.o -lpthread -lrt -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
 echo "$OUT/libyouth_icp.so"
