@@ -141,7 +141,8 @@ int youth_icp_align_batch(const int16_t* src, const int16_t* dst, int n_pairs,
                           float* T_out, int32_t* assoc_out);
 
 /* Context: device workspace sized for max_frames frames of W x H (target
- * records + depth staging).  The pair API needs n_pairs <= max_frames, the
+ * records + depth staging); 3 <= W, H <= 16384 and W*H <= 2^26 (EINVAL
+ * otherwise).  The pair API needs n_pairs <= max_frames, the
  * sequence API n_frames - 1 <= max_frames, the one-shot host API stages
  * 2 * n_pairs depth frames. */
 youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,

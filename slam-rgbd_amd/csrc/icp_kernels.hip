@@ -62,6 +62,8 @@ constexpr int kNeq = YOUTH_NEQ;
 // apart so the contended dequeue atomic shares no line with the polled flag.
 constexpr int kQHead = 0, kQError = 32, kQSpins = 64, kQWaited = 96, kQWords = 128;
 
+typedef float f4v __attribute__((ext_vector_type(4)));  // a gathered {z, nx, ny, nz} record
+
 struct Intr {
     float fx, fy, cx, cy, ds;
 };
@@ -123,7 +125,7 @@ template <bool kFast>
 __device__ __forceinline__ void backproject(int d, int u, int v, const Intr& K,
                                             const FastK& F, float& x, float& y, float& z)
 {
-    const float zz = d > 0 ? bp_div<kFast>((float)d, K.ds, F.rds) : 0.0f;
+    const float zz = bp_div<kFast>((float)max(d, 0), K.ds, F.rds);  // d <= 0: 0/ds = +0
     x = bp_div<kFast>(((float)u - K.cx) * zz, K.fx, F.rfx);
     y = bp_div<kFast>(((float)v - K.cy) * zz, K.fy, F.rfy);
     z = zz;
@@ -300,6 +302,7 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const int16_t* __restrict
             X[2 * P + i] = pz;
         }
         float nx = 0.0f, ny = 0.0f, nz = 0.0f;
+        bool has_n = false;
         const bool inner = gx > 0 && gy > 0 && gx < W - 1 && gy < H - 1;
         if (inner) {
             const float zl = sZ[ly][lx - 1], zr = sZ[ly][lx + 1];
@@ -320,6 +323,7 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const int16_t* __restrict
                     nx = cx / len;
                     ny = cy / len;
                     nz = cz / len;
+                    has_n = true;
                     if (((nx * px + ny * py) + nz * pz) > 0.0f) {
                         nx = -nx;
                         ny = -ny;
@@ -328,7 +332,10 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const int16_t* __restrict
                 }
             }
         }
-        R[i] = make_float4(pz, nx, ny, nz);
+        // a target without a normal is stored as z = 0 ("invalid target"):
+        // the spec's two tests "target valid" and "normal valid" become the
+        // one tz > 0 test in the pixel loop (the Z plane keeps pz)
+        R[i] = make_float4(has_n ? pz : 0.0f, nx, ny, nz);
     }
 }
 
@@ -571,12 +578,17 @@ struct PoseState {
 // Accumulate source pixels [start, end) of one pair into acc (spec a7-a9).
 template <bool kAssoc, bool kFast, bool kAligned>
 __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
-                                                 const float4* __restrict__ rec,
+                                                 const float4* __restrict__ rec, int rec_bytes,
                                                  const float* __restrict__ T, int start, int end,
                                                  int W, int H, const Intr& K, const FastK& F,
                                                  float thr2, double* acc,
                                                  int32_t* __restrict__ arow)
 {
+    // the pair's target records through a buffer descriptor (wave-uniform
+    // base): a gather costs one 32-bit byte offset instead of 64-bit address
+    // arithmetic
+    const __amdgpu_buffer_rsrc_t rrec = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float4*>(rec), (short)0, rec_bytes, 0x00020000);
     // (u0, v0) of pixel i advance incrementally (no integer division per
     // step); with kAligned (W % 4 == 0, i % 4 == 0) a lane's four pixels
     // share one row.  Conditions combine with '&' so the compiler emits
@@ -625,7 +637,9 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
             in[q] = vz & (uu >= 0.0f) & (uu < (float)W) & (vv >= 0.0f) & (vv < (float)H);
             fu[q] = in[q] ? uu : 0.0f;
             fv[q] = in[q] ? vv : 0.0f;
-            j[q] = (int)fv[q] * W + (int)fu[q];  // 0 when !in
+            // 0 when !in; v', W <= 16384 (youth_icp_create): the 24-bit
+            // multiply is exact and full rate
+            j[q] = (int)__umul24((unsigned)(int)fv[q], (unsigned)W) + (int)fu[q];
         }
         u0 += stepU;
         v0 += stepV;
@@ -634,9 +648,11 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
             ++v0;
         }
         // four 16-byte fetches back to back
-        float4 t[4];
+        f4v t[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) t[q] = rec[j[q]];
+        for (int q = 0; q < 4; ++q)
+            t[q] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rrec, j[q] * 16,
+                                                                                 0, 0));
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const float tz = t[q].x;
@@ -645,12 +661,14 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
             const float nx = t[q].y, ny = t[q].z, nz = t[q].w;
             const float dx = qx[q] - tx, dy = qy[q] - ty, dz = qz[q] - tz;
             const float d2 = (dx * dx + dy * dy) + dz * dz;
-            const bool nvalid = (nx != 0.0f) | (ny != 0.0f) | (nz != 0.0f);
-            const bool ok = in[q] & (tz > 0.0f) & nvalid & (d2 < thr2);
+            // target valid AND normal valid: k_prep stores z = 0 for a target
+            // without a normal, so tz > 0 is both tests
+            const bool ok = in[q] & (tz > 0.0f) & (d2 < thr2);
             if (kAssoc && (i + q) < end) arow[i + q] = ok ? j[q] : -1;
-            // spec a8: r = n.(P' - P_t); J = [P' x n, n]  (zeros when unmatched)
+            // spec a8: r = n.(P' - P_t); J = [P' x n, n]  (zeros when unmatched:
+            // with the masked normal r is +-0, which leaves every fp64 sum unchanged)
             const float n0 = ok ? nx : 0.0f, n1 = ok ? ny : 0.0f, n2 = ok ? nz : 0.0f;
-            const float r = ok ? (nx * dx + ny * dy) + nz * dz : 0.0f;
+            const float r = (n0 * dx + n1 * dy) + n2 * dz;
             float Jf[6];
             Jf[0] = qy[q] * n2 - qz[q] * n1;
             Jf[1] = qz[q] * n0 - qx[q] * n2;
@@ -726,8 +744,8 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce(
     const int start = b * chunk;
     const int end = min(start + chunk, N);
     int32_t* arow = kAssoc ? assoc + (size_t)p * N : nullptr;
-    accumulate_chunk<kAssoc, kFast, kAligned>(sD, rec, T, start, end, W, H, K, F, thr2, acc,
-                                              arow);
+    accumulate_chunk<kAssoc, kFast, kAligned>(sD, rec, (int)(P * sizeof(float4)), T, start, end,
+                                              W, H, K, F, thr2, acc, arow);
     // wave reduce-scatter, then the four waves in fixed order through LDS
     const int wave = threadIdx.x >> 6;
     {
@@ -947,8 +965,9 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
         const int start = c * is.chunk;
         const int end = min(start + is.chunk, N);
         accumulate_chunk<false, kFast, kAligned>(dsrc + (size_t)(pm.src0 + p) * N,
-                                                 recs + (size_t)(pm.tgt0 + p) * P, T, start,
-                                                 end, W, H, K, F, thr2, acc, nullptr);
+                                                 recs + (size_t)(pm.tgt0 + p) * P,
+                                                 (int)(P * sizeof(float4)), T, start, end, W, H,
+                                                 K, F, thr2, acc, nullptr);
         {
             double tot;
             wave_reduce_scatter(acc, lane, tot);
@@ -1448,7 +1467,10 @@ void youth_icp_destroy(youth_icp_ctx* c)
 youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
                                 const youth_intrinsics* K, const youth_icp_params* P)
 {
-    if (W < 3 || H < 3 || max_frames < 2 || (long long)W * H > (1LL << 30)) {
+    // W, H <= 16384 and W*H <= 2^26: pixel indices fit the pixel loop's 24-bit
+    // multiply and a target frame's records (16 B/px) its 32-bit buffer offsets
+    if (W < 3 || H < 3 || W > 16384 || H > 16384 || max_frames < 2 ||
+        (long long)W * H > (1LL << 26)) {
         set_error(YOUTH_EINVAL, "youth_icp_create: bad size %dx%d", W, H);
         return nullptr;
     }
