@@ -118,8 +118,8 @@ class Run:
                     per_iter = tj.get("hbm_bytes_per_iteration", tj.get("hbm_bytes_per_launch"))
                     traffic = per_iter * iters_per_launch
                     src = os.path.relpath(self.a.traffic_json, ROOT)
-                    if "valu_issue_frac" in tj:   # PMC SQ pass of the same kernel
-                        valu = {k: tj[k] for k in ("valu_issue_frac",
+                    if "valu_cycles_per_instruction" in tj:   # PMC SQ pass, same kernel
+                        valu = {k: tj[k] for k in ("valu_cycles_per_instruction",
                                                    "valu_lane_ops_per_px_iteration",
                                                    "effective_clock_ghz") if k in tj}
             except (OSError, ValueError, TypeError):

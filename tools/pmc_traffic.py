@@ -10,9 +10,12 @@ gfx950 correction, re-calibrated here: tools/kbench's k_stream_read of a known
 VALU issue: when the SQ pass holds SQ_INSTS_VALU and GRBM_GUI_ACTIVE, also
   effective clock = GRBM_GUI_ACTIVE / n_XCD / kernel duration (MI355X_MICROARCH.md
                     "DVFS give-back": rocprofv3 sums GRBM over the 8 XCDs),
-  VALU issue fraction = SQ_INSTS_VALU x 4 cycles / (SIMDs x GRBM_GUI_ACTIVE / n_XCD)
-(a wave64 VALU instruction occupies its SIMD16 for 4 cycles; fp64 FMA is
-full rate on gfx950).  SIMD count from the pass's agent_info.csv.
+  VALU cycles per instruction = SIMDs x (GRBM_GUI_ACTIVE / n_XCD) / SQ_INSTS_VALU,
+i.e. how many SIMD cycles the kernel spends per issued VALU wave-instruction;
+compare with the per-form issue costs of tools/valu_rate (about 2.4 cycles
+for 2-operand fp32/int ops, 4 for fp64 FMA, converts, compares, selects and
+packed ops): a value near the mix's cost means the kernel is issue-bound.
+SIMD count from the pass's agent_info.csv.
 
 usage: tools/pmc_traffic.py <profile_root> <out.json> <pairs> <width> <height> [iters]
 (iters: ICP iterations each k_icp launch covers; 1 for per-iteration k_reduce)
@@ -57,7 +60,7 @@ def main():
         cyc = r["GRBM_GUI_ACTIVE"] / N_XCD
         doc["valu_wave_instructions_per_launch"] = r["SQ_INSTS_VALU"]
         doc["valu_lane_ops_per_px_iteration"] = r["SQ_INSTS_VALU"] * 64 / (px * iters)
-        doc["valu_issue_frac"] = r["SQ_INSTS_VALU"] * 4.0 / (simds * cyc)
+        doc["valu_cycles_per_instruction"] = simds * cyc / r["SQ_INSTS_VALU"]
         doc["gpu_cycles_per_launch"] = cyc
         doc["simds"] = simds
         durs = []
