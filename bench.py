@@ -69,10 +69,17 @@ class Run:
         self.a = a
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
-        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        # one process per GPU; ranks beyond the visible devices wrap (only for a
+        # rehearsal on fewer GPUs with YOUTH_BENCH_BACKEND=gloo: RCCL needs one
+        # device per rank)
+        self.local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
         torch.cuda.set_device(self.local)
         if self.world > 1:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            backend = os.environ.get("YOUTH_BENCH_BACKEND", "nccl")   # nccl = RCCL over xGMI
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+            else:
+                dist.init_process_group(backend)
 
     def barrier_sync(self):
         torch.cuda.synchronize()
@@ -94,7 +101,8 @@ class Run:
         kt = {k: ctx.get_timing(i) for i, k in enumerate(("k_reduce", "k_solve", "k_prep"))}
         ctx.set_timing(False)
         if self.world > 1:
-            t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+            dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
         return elapsed, kt

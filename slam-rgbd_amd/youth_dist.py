@@ -44,9 +44,11 @@ def gather_poses(local: torch.Tensor, world: int) -> torch.Tensor:
                       device=local.device)
     if dist.get_backend() == "nccl":
         dist.all_gather_into_tensor(out, local.contiguous())
-    else:
-        parts = list(out.chunk(world))
-        dist.all_gather(parts, local.contiguous())
+    else:  # gloo: host tensors (CPU tests; the one-GPU rehearsal of bench.py)
+        host = local.detach().cpu().contiguous()
+        parts = list(torch.empty((world,) + tuple(host.shape), dtype=host.dtype).unbind(0))
+        dist.all_gather(parts, host)
+        out.copy_(torch.cat(parts).to(out.device))
     return out
 
 
