@@ -112,32 +112,6 @@ int main(int argc, char** argv)
         {"prod fast aligned tb1024", 1024, 18, PROD(k_reduce<false, true, true, false>)},
         {"prod fast aligned tb8192", 8192, 18, PROD(k_reduce<false, true, true, false>)},
         {"prod ieee aligned tb2048", 2048, 18, PROD(k_reduce<false, false, true, false>)},
-        {"v5 packed pairs tb2048", 2048, 18, [=](dim3 g, int chunk, double* part) {
-             hipLaunchKernelGGL(k_reduce_v5<true>, g, dim3(kRedThreads), 0, st,
-                                (const int16_t*)d_src, (const float4*)rec, Pp, pm_prod, W, H, Ki,
-                                Fk, thr2, chunk, part, T32);
-         }},
-        {"pf depth-prefetch tb2048", 2048, 18, [=](dim3 g, int chunk, double* part) {
-             hipLaunchKernelGGL((k_reduce_pf<true, true>), g, dim3(kRedThreads), 0, st,
-                                (const int16_t*)d_src, (const float4*)rec, Pp, pm_prod, W, H, Ki,
-                                Fk, thr2, chunk, part, T32);
-         }},
-        {"lds depth-staged tb2048", 2048, 18, [=](dim3 g, int chunk, double* part) {
-             hipLaunchKernelGGL((k_reduce_lds<true, true>), g, dim3(kRedThreads), chunk * 2, st,
-                                (const int16_t*)d_src, (const float4*)rec, Pp, pm_prod, W, H, Ki,
-                                Fk, thr2, chunk, part, T32);
-         }},
-        {"lds depth-staged tb4096", 4096, 18, [=](dim3 g, int chunk, double* part) {
-             hipLaunchKernelGGL((k_reduce_lds<true, true>), g, dim3(kRedThreads), chunk * 2, st,
-                                (const int16_t*)d_src, (const float4*)rec, Pp, pm_prod, W, H, Ki,
-                                Fk, thr2, chunk, part, T32);
-         }},
-        {"pf depth-prefetch tb4096", 4096, 18, [=](dim3 g, int chunk, double* part) {
-             hipLaunchKernelGGL((k_reduce_pf<true, true>), g, dim3(kRedThreads), 0, st,
-                                (const int16_t*)d_src, (const float4*)rec, Pp, pm_prod, W, H, Ki,
-                                Fk, thr2, chunk, part, T32);
-         }},
-        // streaming-read calibration over 28 B/px x pixels x pairs
         {"s0 stream dwordx4 28B/px", 2048, 28, [=](dim3, int, double* part) {
              hipLaunchKernelGGL(k_stream_read, dim3(2048), dim3(256), 0, st, (const float4*)d_big,
                                 (size_t)28 * N * n / 16, (float*)part);
