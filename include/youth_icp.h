@@ -202,6 +202,15 @@ int youth_icp_get_sched_stats(youth_icp_ctx* ctx, unsigned* spins,
 int youth_icp_selftest_projdiv(int device, long long n, unsigned long long seed,
                                long long* bit_mismatches, long long* proj_mismatches);
 
+/* Self-test of the target-normal normalisation's fast path (correctly rounded
+ * sqrt without rescaling, three quotients sharing one reciprocal) against
+ * IEEE sqrtf and division: *sqrt_mismatches over every fp32 in [2^-96, 2^118]
+ * (must be 0), *quot_mismatches bitwise over n random vectors that take the
+ * fast path (must be 0), *fast_cases = how many did. */
+int youth_icp_selftest_normalize(int device, long long n, unsigned long long seed,
+                                 long long* sqrt_mismatches, long long* quot_mismatches,
+                                 long long* fast_cases);
+
 /* --- Stage-level entry points (validation / parity tests) --------------- */
 
 /* Depth -> XYZ planes (+ normals when want_normals) for n_frames host frames.

@@ -118,6 +118,39 @@ __device__ __forceinline__ bool proj_den_ok(float den)
     return (den >= 0x1p-60f) & (den <= 0x1p60f);
 }
 
+// Spec a6's normalisation n = c / sqrtf(|c|^2) on its common range, bit for
+// bit.  hipcc's correctly rounded sqrtf is  x' = x < 2^-96 ? x 2^32 : x;
+// s = v_sqrt(x'); s -= (fma(-(s-1ulp), s, x') <= 0); s += (fma(-(s+1ulp), s,
+// x') > 0); unscale; return x for +-0 / +inf (`make asm`).  For x in
+// [2^-96, 2^118] the scaling and the class fix-up are identities, leaving
+// the sequence below.  The three quotients then share one reciprocal
+// (proj_div_one): len = sqrt(x) is in [2^-48, 2^59] and |c_i| <= ~len, so
+// div_scale rescales no operand when |c_i| >= 2^-64; c_i = 0
+// is exact through the sign: RN(c/len) = copysign(RN(|c|/len), c).  Callers
+// take the IEEE expressions when norm_fast_ok is false.
+// youth_icp_selftest_normalize checks both against IEEE on device.
+__device__ __forceinline__ float sqrt_rn_mid(float x)
+{
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sdn = __uint_as_float(__float_as_uint(s) - 1u);
+    const float sup = __uint_as_float(__float_as_uint(s) + 1u);
+    const float t = fmaf(-sdn, s, x) <= 0.0f ? sdn : s;
+    return fmaf(-sup, s, x) > 0.0f ? sup : t;
+}
+__device__ __forceinline__ bool norm_comp_ok(float c)
+{
+    return !((fabsf(c) < 0x1p-64f) & (c != 0.0f));
+}
+__device__ __forceinline__ bool norm_fast_ok(float len2, float cx, float cy, float cz)
+{
+    return (len2 >= 0x1p-96f) && (len2 <= 0x1p118f) && norm_comp_ok(cx) && norm_comp_ok(cy) &&
+           norm_comp_ok(cz);
+}
+__device__ __forceinline__ float norm_div(float c, float len, float r)
+{
+    return copysignf(proj_div_one(fabsf(c), len, r), c);
+}
+
 // viewerModule.c:341-345 with explicit intrinsics (bit-identical to the
 // viewer for cx = W/2, cy = H/2, f = 570.3f, ds = 1000.0f):
 //   valid iff d > 0;  z = d / ds;  x = ((u - cx) z) / fx;  y = ((v - cy) z) / fy
@@ -221,6 +254,50 @@ __global__ void k_selftest_projdiv(unsigned long long n, unsigned long long seed
     if (b1) atomicAdd(bad + 1, b1);
 }
 
+// Self-test of k_prep's fast normalisation (sqrt_rn_mid, norm_div):
+//   bad[0]: sqrt_rn_mid(x) != sqrtf(x) over EVERY fp32 x in [2^-96, 2^118];
+//   bad[1]: bitwise differences of (nx, ny, nz) vs c / sqrtf(len2) over `n`
+//           random vectors (components of mixed magnitude down to 2^-110,
+//           each +-0 with probability 1/8), wherever norm_fast_ok holds;
+//   bad[2]: number of random vectors that took the fast path (coverage).
+__global__ void k_selftest_normalize(unsigned long long n, unsigned long long seed,
+                                     unsigned long long* bad)
+{
+    unsigned long long b0 = 0, b1 = 0, nf = 0;
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+    const unsigned long long tid = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    constexpr unsigned kLo = 0x0F800000u, kHi = 0x7A800000u;  // 2^-96, 2^118
+    for (unsigned long long b = kLo + tid; b <= kHi; b += stride) {
+        const float x = __uint_as_float((unsigned)b);
+        b0 += __float_as_uint(sqrt_rn_mid(x)) != __float_as_uint(sqrtf(x));
+    }
+    for (unsigned long long i = tid; i < n; i += stride) {
+        unsigned long long st = seed ^ (i * 0xD1B54A32D192ED03ull);
+        const int e0 = (int)(sm64(st) % 131) - 70;  // leading exponent in [-70, 60]
+        float c[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const unsigned long long r = sm64(st);
+            const int e = max(e0 - (int)((r >> 32) % 48), -126);
+            const unsigned sign = (unsigned)(r >> 63) << 31;
+            c[k] = ((r >> 56) & 7) == 0
+                       ? __uint_as_float(sign)
+                       : __uint_as_float(sign | (unsigned)((e + 127) << 23) |
+                                         (unsigned)(r & 0x7FFFFF));
+        }
+        const float len2 = (c[0] * c[0] + c[1] * c[1]) + c[2] * c[2];
+        if (!(len2 > 0.0f) || !norm_fast_ok(len2, c[0], c[1], c[2])) continue;
+        ++nf;
+        const float len = sqrt_rn_mid(len2), r = proj_recip(len), ref = sqrtf(len2);
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            b1 += __float_as_uint(norm_div(c[k], len, r)) != __float_as_uint(c[k] / ref);
+    }
+    if (b0) atomicAdd(bad + 0, b0);
+    if (b1) atomicAdd(bad + 1, b1);
+    if (nf) atomicAdd(bad + 2, nf);
+}
+
 // ------------------------------------------------------------------ k_prep --
 // grid (ceil(W/64), ceil(H/16), n_frames): frame f reads depth + f*N and
 // writes the target records of workspace frame out0 + f (and, when xyz is
@@ -319,10 +396,18 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const int16_t* __restrict
                 const float cz = ax * by - ay * bx;
                 const float len2 = (cx * cx + cy * cy) + cz * cz;
                 if (len2 > 0.0f) {
-                    const float len = sqrtf(len2);  // correctly rounded (checked in .s)
-                    nx = cx / len;
-                    ny = cy / len;
-                    nz = cz / len;
+                    if (norm_fast_ok(len2, cx, cy, cz)) {
+                        const float len = sqrt_rn_mid(len2);
+                        const float r = proj_recip(len);
+                        nx = norm_div(cx, len, r);
+                        ny = norm_div(cy, len, r);
+                        nz = norm_div(cz, len, r);
+                    } else {
+                        const float len = sqrtf(len2);  // correctly rounded (checked in .s)
+                        nx = cx / len;
+                        ny = cy / len;
+                        nz = cz / len;
+                    }
                     has_n = true;
                     if (((nx * px + ny * py) + nz * pz) > 0.0f) {
                         nx = -nx;
@@ -1675,6 +1760,34 @@ int youth_icp_selftest_projdiv(int device, long long n, unsigned long long seed,
     if (e != hipSuccess) return set_error(YOUTH_EHIP, "selftest_projdiv: %s", hipGetErrorString(e));
     if (bit_mismatches) *bit_mismatches = (long long)h[0];
     if (proj_mismatches) *proj_mismatches = (long long)h[1];
+    return YOUTH_OK;
+}
+
+int youth_icp_selftest_normalize(int device, long long n, unsigned long long seed,
+                                 long long* sqrt_mismatches, long long* quot_mismatches,
+                                 long long* fast_cases)
+{
+    if (n < 0) return set_error(YOUTH_EINVAL, "selftest_normalize: n < 0");
+    const int ndev = youth_icp_device_count();
+    if (ndev <= 0 || device < 0 || device >= ndev)
+        return set_error(YOUTH_ENODEV, "selftest_normalize: no HIP device %d", device);
+    HIP_TRY(hipSetDevice(device));
+    unsigned long long* d_bad = nullptr;
+    HIP_TRY(hipMalloc(&d_bad, 3 * sizeof(unsigned long long)));
+    unsigned long long h[3] = {0, 0, 0};
+    hipError_t e = hipMemset(d_bad, 0, sizeof(h));
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_selftest_normalize, dim3(8192), dim3(256), 0, 0,
+                           (unsigned long long)n, seed, d_bad);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(h, d_bad, sizeof(h), hipMemcpyDeviceToHost);
+    (void)hipFree(d_bad);
+    if (e != hipSuccess)
+        return set_error(YOUTH_EHIP, "selftest_normalize: %s", hipGetErrorString(e));
+    if (sqrt_mismatches) *sqrt_mismatches = (long long)h[0];
+    if (quot_mismatches) *quot_mismatches = (long long)h[1];
+    if (fast_cases) *fast_cases = (long long)h[2];
     return YOUTH_OK;
 }
 

@@ -101,6 +101,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "youth_icp_selftest_projdiv": (c_int, [c_int, ctypes.c_longlong, ctypes.c_ulonglong,
                                                POINTER(ctypes.c_longlong),
                                                POINTER(ctypes.c_longlong)]),
+        "youth_icp_selftest_normalize": (c_int, [c_int, ctypes.c_longlong, ctypes.c_ulonglong,
+                                                 POINTER(ctypes.c_longlong),
+                                                 POINTER(ctypes.c_longlong),
+                                                 POINTER(ctypes.c_longlong)]),
         "youth_icp_prepare_host": (c_int, [c_void_p, P16, c_int, c_int, PF, PF, PF, PF, PF,
                                            PF]),
         "youth_icp_reduce_host": (c_int, [c_void_p, P16, P16, PF, PI32, PD]),
@@ -406,6 +410,16 @@ def selftest_projdiv(n: int, seed: int = 1, device: int = 0) -> tuple[int, int]:
     b, p = ctypes.c_longlong(0), ctypes.c_longlong(0)
     _check(lib.youth_icp_selftest_projdiv(device, n, seed, ctypes.byref(b), ctypes.byref(p)))
     return b.value, p.value
+
+
+def selftest_normalize(n: int, seed: int = 1, device: int = 0) -> tuple[int, int, int]:
+    """youth_icp_selftest_normalize: (sqrt mismatches over [2^-96, 2^118],
+    quotient mismatches, fast-path cases) of k_prep's fast normalisation vs IEEE."""
+    lib = load_library()
+    s, q, f = ctypes.c_longlong(0), ctypes.c_longlong(0), ctypes.c_longlong(0)
+    _check(lib.youth_icp_selftest_normalize(device, n, seed, ctypes.byref(s), ctypes.byref(q),
+                                            ctypes.byref(f)))
+    return s.value, q.value, f.value
 
 
 def align_batch(src: np.ndarray, dst: np.ndarray, K: Intrinsics | None = None, iters: int = 10,

@@ -319,6 +319,17 @@ def test_projection_division_matches_ieee():
         assert bits == 0 and proj == 0, (seed, bits, proj)
 
 
+def test_normal_normalisation_matches_ieee():
+    """k_prep's fast normalisation (icp_kernels.hip sqrt_rn_mid / norm_div)
+    equals sqrtf and c / sqrtf(|c|^2) bit for bit: the sqrt exhaustively over
+    [2^-96, 2^118], the quotients on 2 x 2^28 random vectors of mixed
+    magnitude with signed zeros (most take the fast path)."""
+    for seed in (1, 0x5EED):
+        sq, quot, fast = youth_icp.selftest_normalize(1 << 28, seed)
+        assert sq == 0 and quot == 0, (seed, sq, quot)
+        assert fast > (1 << 27), fast
+
+
 def test_fastdiv_path_is_bit_identical_to_ieee(monkeypatch):
     """The verified 3-op back-projection divide must change nothing: both
     paths give the same association and bit-identical poses."""
