@@ -160,7 +160,7 @@ def run_pairs(R):
     d_src = torch.from_numpy(src).cuda()
     d_dst = torch.from_numpy(dst).cuda()
     poses = torch.zeros((n, 16), dtype=torch.float32, device="cuda")
-    ctx = youth_icp.IcpContext(W, H, n, iters=a.iters, device=R.local)
+    ctx = youth_icp.IcpContext(W, H, max(n, 2), iters=a.iters, device=R.local)
     stream = torch.cuda.current_stream().cuda_stream
 
     def step():

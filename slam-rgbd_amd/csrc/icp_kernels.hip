@@ -58,11 +58,18 @@ constexpr int kLdsH = kTileH + 2;
 constexpr int kRedThreads = 256;
 constexpr int kRedStep = kRedThreads * 4;  // pixels per workgroup loop step
 constexpr int kNeq = YOUTH_NEQ;
+// k_icp's chunk partials: rows of 30 doubles (29 + a zero pad, 240 B) so the
+// last arriver reads them as 16-byte pieces; kSumCols interleaved columns of
+// chunks are summed in parallel, then the column sums in column order.
+constexpr int kPartStride = 30;
+constexpr int kPieces = kPartStride / 2;  // 16-byte pieces per row
+constexpr int kSumCols = 16;              // kSumCols * kPieces <= kRedThreads
 // Persistent-queue words (unsigned index into ctx->d_head), one 128-B line
 // apart so the contended dequeue atomic shares no line with the polled flag.
 constexpr int kQHead = 0, kQError = 32, kQSpins = 64, kQWaited = 96, kQWords = 128;
 
 typedef float f4v __attribute__((ext_vector_type(4)));  // a gathered {z, nx, ny, nz} record
+typedef unsigned u4v __attribute__((ext_vector_type(4)));  // two doubles, raw bits
 
 struct Intr {
     float fx, fy, cx, cy, ds;
@@ -1016,7 +1023,10 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
                                                     IterState is)
 {
     __shared__ double red[kRedThreads / 64][kNeq];
+    __shared__ double colsum[kSumCols][kPartStride];
+    __shared__ double sh_T64[12];
     __shared__ int sh_item;
+    __shared__ int sh_last;
     __shared__ float sh_T[12];
     const int N = W * H;
     const int per_iter = is.n_pairs * is.nblk;
@@ -1063,53 +1073,72 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
         if (wave == 0) {
             // ---- publish this chunk's partial, take the arrival ticket
             double sum = 0.0;
-            if (lane < kNeq) {
+            if (lane < kPartStride) {
+                if (lane < kNeq)
 #pragma unroll
-                for (int w = 0; w < kRedThreads / 64; ++w) sum += red[w][lane];
-                st_u64_sc1(partials + ((size_t)p * is.nblk + c) * kNeq + lane,
+                    for (int w = 0; w < kRedThreads / 64; ++w) sum += red[w][lane];
+                st_u64_sc1(partials + ((size_t)p * is.nblk + c) * kPartStride + lane,
                            (unsigned long long)__double_as_longlong(sum));
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            unsigned ticket = 0;
-            if (lane == 0)
-                ticket = __hip_atomic_fetch_add(is.arrivals + (size_t)p * is.iters + k, 1u,
-                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ticket = __shfl(ticket, 0, 64);
-            if (ticket == (unsigned)is.nblk - 1) {
-                // ---- last arriver of (p, k): fixed-order sum (as k_solve),
-                // solve, publish the pose, then the epoch.  The fp64 pose
-                // (lanes 32..43) is loaded with the partials (batches of 16).
-                const double* base = partials + (size_t)p * is.nblk * kNeq;
-                const int half = (is.nblk + 1) >> 1;
-                const int kk = lane & 31;
-                double Tl = 0.0;
-                if (lane >= 32 && lane < 44)
-                    Tl = __longlong_as_double(
-                        (long long)ld_u64_sc1(is.T64 + (size_t)p * 16 + (lane - 32)));
-                double t = 0.0;
-                if (kk < kNeq) {
-                    const int b0 = lane < 32 ? 0 : half;
-                    const int b1 = lane < 32 ? half : is.nblk;
-                    for (int bb = b0; bb < b1; bb += 16) {
-                        double v[16];
+            if (lane == 0) {
+                const unsigned ticket = __hip_atomic_fetch_add(
+                    is.arrivals + (size_t)p * is.iters + k, 1u, __ATOMIC_RELAXED,
+                    __HIP_MEMORY_SCOPE_AGENT);
+                sh_last = ticket == (unsigned)is.nblk - 1;
+            }
+        }
+        __syncthreads();
+        if (__builtin_amdgcn_readfirstlane(sh_last)) {
+            // ---- last arriver of (p, k): every wave sums a share of the
+            // pair's partials (sc1 16-byte loads, one batch for <= 256
+            // chunks): thread (col j, piece q) adds rows j, j + 16, ... in
+            // order; then wave 0 adds the 16 column sums in order, solves,
+            // publishes the pose, then the epoch.
+            const __amdgpu_buffer_rsrc_t rpart = __builtin_amdgcn_make_buffer_rsrc(
+                partials + (size_t)p * is.nblk * kPartStride, (short)0,
+                is.nblk * kPartStride * (int)sizeof(double), 0x00020000);
+            const int t = threadIdx.x;
+            const int j = t / kPieces, q = t - j * kPieces;
+            if (j < kSumCols) {
+                double s0 = 0.0, s1 = 0.0;
+                for (int bb = j; bb < is.nblk; bb += 16 * kSumCols) {
+                    u4v v[16];
 #pragma unroll
-                        for (int q = 0; q < 16; ++q)
-                            v[q] = bb + q < b1
-                                       ? __longlong_as_double((long long)ld_u64_sc1(
-                                             base + (size_t)(bb + q) * kNeq + kk))
-                                       : 0.0;
+                    for (int i = 0; i < 16; ++i) {
+                        const int b = bb + i * kSumCols;
+                        // aux 16 = sc1 (bypass this CU's L1: written by other CUs)
+                        v[i] = b < is.nblk ? __builtin_bit_cast(
+                                                 u4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                                          rpart, (b * kPartStride + 2 * q) * 8, 0,
+                                                          16))
+                                           : u4v{0u, 0u, 0u, 0u};
+                    }
 #pragma unroll
-                        for (int q = 0; q < 16; ++q) t += v[q];
+                    for (int i = 0; i < 16; ++i) {
+                        s0 += __hiloint2double((int)v[i].y, (int)v[i].x);
+                        s1 += __hiloint2double((int)v[i].w, (int)v[i].z);
                     }
                 }
-                t += __shfl_down(t, 32, 64);
+                colsum[j][2 * q] = s0;
+                colsum[j][2 * q + 1] = s1;
+            } else if (t >= kSumCols * kPieces && t < kSumCols * kPieces + 12) {
+                sh_T64[t - kSumCols * kPieces] = __longlong_as_double((long long)ld_u64_sc1(
+                    is.T64 + (size_t)p * 16 + (t - kSumCols * kPieces)));
+            }
+            __syncthreads();
+            if (wave == 0) {
+                double tsum = 0.0;
+                if (lane < kNeq)
+#pragma unroll
+                    for (int jj = 0; jj < kSumCols; ++jj) tsum += colsum[jj][lane];
                 double neq[kNeq];
 #pragma unroll
-                for (int q = 0; q < kNeq; ++q) neq[q] = __shfl(t, q, 64);
-                double Tm[16];
-#pragma unroll
-                for (int q = 0; q < 12; ++q) Tm[q] = __shfl(Tl, 32 + q, 64);
+                for (int qq = 0; qq < kNeq; ++qq) neq[qq] = __shfl(tsum, qq, 64);
                 if (lane == 0) {
+                    double Tm[16];
+#pragma unroll
+                    for (int qq = 0; qq < 12; ++qq) Tm[qq] = sh_T64[qq];
                     if (is.stats) {
                         is.stats[((size_t)p * is.iters + k) * 2 + 0] = neq[28];
                         is.stats[((size_t)p * is.iters + k) * 2 + 1] = neq[27];
@@ -1119,24 +1148,24 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
                     if (st == 0) se3_exp_left(xi, Tm);
                     if (st) __hip_atomic_fetch_or(is.status + p, st, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
-                    for (int q = 0; q < 12; ++q)
-                        st_u64_sc1(is.T64 + (size_t)p * 16 + q,
-                                   (unsigned long long)__double_as_longlong(Tm[q]));
-                    for (int q = 0; q < 12; q += 2)
-                        st_u64_sc1(is.T32 + (size_t)p * 12 + q,
-                                   (unsigned long long)__float_as_uint((float)Tm[q]) |
-                                       ((unsigned long long)__float_as_uint((float)Tm[q + 1])
+                    for (int qq = 0; qq < 12; ++qq)
+                        st_u64_sc1(is.T64 + (size_t)p * 16 + qq,
+                                   (unsigned long long)__double_as_longlong(Tm[qq]));
+                    for (int qq = 0; qq < 12; qq += 2)
+                        st_u64_sc1(is.T32 + (size_t)p * 12 + qq,
+                                   (unsigned long long)__float_as_uint((float)Tm[qq]) |
+                                       ((unsigned long long)__float_as_uint((float)Tm[qq + 1])
                                         << 32));
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     st_u32_sc1(is.epoch + p, (unsigned)(k + 1));
                 }
             }
-            // ---- next item (this workgroup has published: waiting is safe)
-            if (lane == 0) {
-                const int next = (int)__hip_atomic_fetch_add(is.head, 1u, __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_AGENT);
-                sh_item = icp_claim(is, next, total, per_iter, sh_T);
-            }
+        }
+        // ---- next item (this workgroup has published: waiting is safe)
+        if (threadIdx.x == 0) {
+            const int next = (int)__hip_atomic_fetch_add(is.head, 1u, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+            sh_item = icp_claim(is, next, total, per_iter, sh_T);
         }
         __syncthreads();
     }
@@ -1425,7 +1454,7 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
     if (persistent) {
         int chunk = 0;
         const int nb = reduce_geometry(c, n_pairs, &chunk);
-        rc = ensure_partials(c, (size_t)nb * n_pairs * kNeq);
+        rc = ensure_partials(c, (size_t)nb * n_pairs * kPartStride);
         if (rc) return rc;
         const bool aligned = (reinterpret_cast<uintptr_t>(dsrc) % 8 == 0) && (c->W % 4 == 0);
         const int var = (c->fast ? 2 : 0) | (aligned ? 1 : 0);
@@ -1556,7 +1585,10 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
     // multiply and a target frame's records (16 B/px) its 32-bit buffer offsets
     if (W < 3 || H < 3 || W > 16384 || H > 16384 || max_frames < 2 ||
         (long long)W * H > (1LL << 26)) {
-        set_error(YOUTH_EINVAL, "youth_icp_create: bad size %dx%d", W, H);
+        set_error(YOUTH_EINVAL,
+                  "youth_icp_create: bad size %dx%d / max_frames %d (need 3 <= W, H <= 16384, "
+                  "W*H <= 2^26, max_frames >= 2)",
+                  W, H, max_frames);
         return nullptr;
     }
     const int ndev = youth_icp_device_count();
