@@ -792,25 +792,84 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
 // fp64 exchanges number 16 + 8 + 4 + 2 + 1 + 1 = 32 instead of 29 x 6 for a
 // symmetric butterfly.  On exit lane 2q and 2q+1 both hold the wave total of
 // value q (q < kNeq); the summation tree is fixed, so results are
-// deterministic.  Shared by k_reduce and k_icp.
+// deterministic.  Shared by k_reduce, k_icp and k_icp_coop.
+//   m = 32, 16: v_permlane32_swap / v_permlane16_swap exchange the upper
+//     half-wave (odd rows) of one register with the lower half (even rows) of
+//     another.  With vdst = v[q] and src = v[q+h], each lane is left holding
+//     the value it keeps in one register and its partner's send in the other,
+//     so v[q] = D + S with no select (keep + recv, commutative: bitwise the
+//     same as the shuffle form).
+//   m = 8, 2, 1: DPP (row_ror:8, quad_perm) moves; m = 4: ds_swizzle xor.
+// No LDS bpermute; the partners (lane ^ m) and the add order are unchanged,
+// so the sums are bit-identical to the shuffle form.
+__device__ __forceinline__ double join64(unsigned lo, unsigned hi)
+{
+    return __hiloint2double((int)hi, (int)lo);
+}
+__device__ __forceinline__ unsigned lo32(double x) { return (unsigned)__double2loint(x); }
+__device__ __forceinline__ unsigned hi32(double x) { return (unsigned)__double2hiint(x); }
+
+// lane `l`'s value in every lane (wave-uniform l: two v_readlane into SGPRs)
+__device__ __forceinline__ double readlane64(double x, int l)
+{
+    return join64((unsigned)__builtin_amdgcn_readlane((int)lo32(x), l),
+                  (unsigned)__builtin_amdgcn_readlane((int)hi32(x), l));
+}
+
+template <int kM>
+__device__ __forceinline__ double xchg_small(double x)
+{
+    int lo = (int)lo32(x), hi = (int)hi32(x);
+    if (kM == 8) {
+        lo = __builtin_amdgcn_update_dpp(0, lo, 0x128, 0xf, 0xf, false);  // row_ror:8
+        hi = __builtin_amdgcn_update_dpp(0, hi, 0x128, 0xf, 0xf, false);
+    } else if (kM == 4) {
+        lo = __builtin_amdgcn_ds_swizzle(lo, 0x1F | (4 << 10));  // bit mode, xor 4
+        hi = __builtin_amdgcn_ds_swizzle(hi, 0x1F | (4 << 10));
+    } else if (kM == 2) {
+        lo = __builtin_amdgcn_update_dpp(0, lo, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+        hi = __builtin_amdgcn_update_dpp(0, hi, 0x4E, 0xf, 0xf, false);
+    } else {
+        lo = __builtin_amdgcn_update_dpp(0, lo, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+        hi = __builtin_amdgcn_update_dpp(0, hi, 0xB1, 0xf, 0xf, false);
+    }
+    return join64((unsigned)lo, (unsigned)hi);
+}
+
+template <int kM>
+__device__ __forceinline__ void rs_stage_small(double* v, int lane)
+{
+    constexpr int h = kM / 2;
+    const bool up = (lane & kM) != 0;
+#pragma unroll
+    for (int q = 0; q < h; ++q) {
+        const double send = up ? v[q] : v[q + h];
+        const double keep = up ? v[q + h] : v[q];
+        v[q] = keep + xchg_small<kM>(send);
+    }
+}
+
 __device__ __forceinline__ void wave_reduce_scatter(const double* acc, int lane, double& total)
 {
     double v[32];
 #pragma unroll
     for (int q = 0; q < 32; ++q) v[q] = q < kNeq ? acc[q] : 0.0;
 #pragma unroll
-    for (int st = 0; st < 5; ++st) {
-        const int m = 32 >> st;
-        const int h = 16 >> st;
-        const bool up = (lane & m) != 0;
-#pragma unroll
-        for (int q = 0; q < h; ++q) {
-            const double send = up ? v[q] : v[q + h];
-            const double keep = up ? v[q + h] : v[q];
-            v[q] = keep + __shfl_xor(send, m, 64);
-        }
+    for (int q = 0; q < 16; ++q) {  // m = 32
+        const auto l = __builtin_amdgcn_permlane32_swap(lo32(v[q]), lo32(v[q + 16]), false, false);
+        const auto h = __builtin_amdgcn_permlane32_swap(hi32(v[q]), hi32(v[q + 16]), false, false);
+        v[q] = join64(l[0], h[0]) + join64(l[1], h[1]);
     }
-    total = v[0] + __shfl_xor(v[0], 1, 64);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {  // m = 16
+        const auto l = __builtin_amdgcn_permlane16_swap(lo32(v[q]), lo32(v[q + 8]), false, false);
+        const auto h = __builtin_amdgcn_permlane16_swap(hi32(v[q]), hi32(v[q + 8]), false, false);
+        v[q] = join64(l[0], h[0]) + join64(l[1], h[1]);
+    }
+    rs_stage_small<8>(v, lane);
+    rs_stage_small<4>(v, lane);
+    rs_stage_small<2>(v, lane);
+    total = v[0] + xchg_small<1>(v[0]);
 }
 
 template <bool kAssoc, bool kFast, bool kAligned, bool kFuse>
@@ -1134,7 +1193,7 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
                     for (int jj = 0; jj < kSumCols; ++jj) tsum += colsum[jj][lane];
                 double neq[kNeq];
 #pragma unroll
-                for (int qq = 0; qq < kNeq; ++qq) neq[qq] = __shfl(tsum, qq, 64);
+                for (int qq = 0; qq < kNeq; ++qq) neq[qq] = readlane64(tsum, qq);
                 if (lane == 0) {
                     double Tm[16];
 #pragma unroll
@@ -1168,6 +1227,343 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
             sh_item = icp_claim(is, next, total, per_iter, sh_T);
         }
         __syncthreads();
+    }
+}
+
+// -------------------------------------------------------------- k_icp_coop --
+// Small batches: C2's single pair and the SLAM tracker's frame-to-frame align
+// (youth_icp_track_frame).  One pair cannot fill the chip, so k_icp's cost
+// there is the chain of memory round trips per iteration (dequeue, pose poll,
+// pose load, cold depth and record loads, ticket, last-arriver solve, pose
+// publish: ~17 us).  This kernel shortens that chain:
+//   * ONE cooperative launch of n_pairs x G co-resident workgroups replaces
+//     k_init + k_icp + k_finish; workgroup b owns chunk c = b % G of pair
+//     p = b / G for every iteration (no queue);
+//   * its source pixels (kSteps x 1024) are loaded and back-projected ONCE
+//     and stay in registers; its record gathers hit the same lines every
+//     iteration (L1/L2-warm);
+//   * per iteration ONE hand-off: each workgroup publishes its partial
+//     (sc1 stores, drained) and adds to one of 8 arrival counters of its pair
+//     (shard = c & 7, one 128-B line each); every workgroup polls the 8
+//     shards, then sums ALL the pair's partials in the fixed column order of
+//     k_icp's last arriver and solves itself.  Identical inputs and code give
+//     every workgroup the identical fp64 pose, so no pose is handed off.
+// Partials are double-buffered by iteration parity: a workgroup writes
+// iteration k+2's row only after every workgroup of its pair published k+1,
+// i.e. finished reading k's rows.  Arrival counters count across iterations
+// (after iteration k shard s holds (k+1) x its workgroup count); this call's
+// counter set and timeout word were zeroed by the previous call, and this
+// call zeroes the next call's (stream order: the set a call uses is never
+// the one it clears).  Co-residency is guaranteed by the cooperative launch;
+// every spin is still bounded (timeout -> YOUTH_STATUS_TIMEOUT, no hang).
+constexpr int kCoopShards = 8;
+constexpr int kCoopShardStride = 32;  // words: one 128-B line per shard
+constexpr int kCoopMaxSteps = 4;
+constexpr int kCoopMaxPairs = 16;     // counter words per set: 16 x 8 x 32
+constexpr int kCoopSetWords = kCoopMaxPairs * kCoopShards * kCoopShardStride + kCoopShardStride;
+constexpr unsigned kCoopSpinMax = 1u << 22;  // polls (~1 us each): seconds, never reached
+
+struct CoopState {
+    const double* T_init;  // [pair][16] or null (identity)
+    double* T64;           // [pair][16]
+    float* T32;            // [pair][12]
+    int32_t* status;       // [pair]
+    double* stats;         // [pair][iters][2]
+    float* T_out;          // [pair][16] fp32 4x4, or null
+    unsigned* set;         // this call's counters [pair][shard * 32] + timeout word
+    unsigned* set_next;    // the next call's: zeroed here
+    unsigned* head_err;    // k_icp's queue words: error/telemetry cleared for get_poses
+    int iters, n_pairs, G, chunk;
+};
+
+// Phase timestamps for tools/coopbench only (never in the product build):
+// thread 0 of every workgroup records s_memrealtime (100 MHz) at 8 points of
+// each iteration into coop_phase[block][iteration][8].
+#ifdef YOUTH_COOP_PHASES
+__device__ unsigned long long* coop_phase;
+#define COOP_MARK(k, slot)                                                           \
+    do {                                                                             \
+        if (threadIdx.x == 0 && coop_phase && (k) < 32)                              \
+            coop_phase[((size_t)blockIdx.x * 32 + (k)) * 8 + (slot)] =               \
+                __builtin_amdgcn_s_memrealtime();                                    \
+    } while (0)
+#else
+#define COOP_MARK(k, slot) \
+    do {                   \
+    } while (0)
+#endif
+
+template <bool kFast, bool kAligned, int kSteps>
+__global__ __launch_bounds__(kRedThreads, 2) void k_icp_coop(const int16_t* __restrict__ dsrc,
+                                                             const float4* __restrict__ recs,
+                                                             size_t P, PairMap pm, int W, int H,
+                                                             Intr K, FastK F, float thr2,
+                                                             double* __restrict__ partials,
+                                                             CoopState cs)
+{
+    __shared__ double red[kRedThreads / 64][kNeq];
+    __shared__ double colsum[kSumCols][kPartStride];
+    __shared__ double sh_T64[12];
+    __shared__ float sh_T[12];
+    __shared__ int sh_stop;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int G = cs.G;
+    const int p = blockIdx.x / G;
+    const int c = blockIdx.x - p * G;
+    const int N = W * H;
+    unsigned* cnt = cs.set + (size_t)p * kCoopShards * kCoopShardStride;
+    unsigned* err = cs.set + (size_t)kCoopMaxPairs * kCoopShards * kCoopShardStride;
+
+    if (blockIdx.x == 0) {
+        for (int i = threadIdx.x; i < kCoopSetWords; i += kRedThreads) st_u32_sc1(cs.set_next + i, 0u);
+        if (threadIdx.x == 0) {
+            st_u32_sc1(cs.head_err + kQError, 0u);
+            st_u32_sc1(cs.head_err + kQSpins, 0u);
+            st_u32_sc1(cs.head_err + kQWaited, 0u);
+        }
+    }
+    if (threadIdx.x < 12) {
+        const double v = cs.T_init ? cs.T_init[(size_t)p * 16 + threadIdx.x]
+                                   : ((threadIdx.x % 5) == 0 ? 1.0 : 0.0);
+        sh_T64[threadIdx.x] = v;
+        sh_T[threadIdx.x] = (float)v;
+    }
+
+    // ---- this workgroup's source pixels, back-projected once (spec a2)
+    const int16_t* sD = dsrc + (size_t)(pm.src0 + p) * N;
+    const int base = c * cs.chunk;
+    float sx[kSteps][4], sy[kSteps][4], sz[kSteps][4];
+#pragma unroll
+    for (int s = 0; s < kSteps; ++s) {
+        const int i = base + s * kRedStep + threadIdx.x * 4;
+        short4 d4 = make_short4(0, 0, 0, 0);
+        if (i < N) d4 = load_depth4<kAligned>(sD, i, N);
+        const int dd[4] = {d4.x, d4.y, d4.z, d4.w};
+        const int ii = i < N ? i : 0;
+        const int v0 = ii / W;
+        const int u0 = ii - v0 * W;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            int u = u0 + q, v = v0;
+            if (!kAligned) {
+                const bool wrap = u >= W;
+                u = wrap ? u - W : u;
+                v = wrap ? v + 1 : v;
+            }
+            backproject<kFast>((i + q) < N ? dd[q] : 0, u, v, K, F, sx[s][q], sy[s][q], sz[s][q]);
+        }
+    }
+    const __amdgpu_buffer_rsrc_t rrec = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float4*>(recs + (size_t)(pm.tgt0 + p) * P), (short)0,
+        (int)(P * sizeof(float4)), 0x00020000);
+    // shard s of this pair holds (k+1) x n_s after iteration k
+    const int my_shard = c & (kCoopShards - 1);
+    const unsigned n_s = lane < kCoopShards ? (unsigned)((G - lane + kCoopShards - 1) / kCoopShards)
+                                            : 0u;
+    int32_t st_acc = 0;
+    bool timeout = false;
+    __syncthreads();
+
+    for (int k = 0; k < cs.iters; ++k) {
+        COOP_MARK(k, 0);
+        float T[12];
+#pragma unroll
+        for (int q = 0; q < 12; ++q)
+            T[q] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sh_T[q])));
+        double acc[kNeq];
+#pragma unroll
+        for (int q = 0; q < kNeq; ++q) acc[q] = 0.0;
+        int nmatch = 0;
+#pragma unroll
+        for (int s = 0; s < kSteps; ++s) {
+            float qx[4], qy[4], qz[4], fu[4], fv[4];
+            bool in[4];
+            int j[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                // spec a7 (same expressions as accumulate_chunk)
+                qx[q] = ((T[0] * sx[s][q] + T[1] * sy[s][q]) + T[2] * sz[s][q]) + T[3];
+                qy[q] = ((T[4] * sx[s][q] + T[5] * sy[s][q]) + T[6] * sz[s][q]) + T[7];
+                qz[q] = ((T[8] * sx[s][q] + T[9] * sy[s][q]) + T[10] * sz[s][q]) + T[11];
+                const bool vz = (sz[s][q] > 0.0f) & (qz[q] > 0.0f);
+                const float qzs = vz ? qz[q] : 1.0f;
+                const float nu = K.fx * qx[q], nv = K.fy * qy[q];
+                float du, dv;
+                if (proj_den_ok(qzs)) {
+                    const float r = proj_recip(qzs);
+                    du = proj_div_one(nu, qzs, r);
+                    dv = proj_div_one(nv, qzs, r);
+                } else {
+                    du = nu / qzs;
+                    dv = nv / qzs;
+                }
+                const float uu = floorf((du + K.cx) + 0.5f);
+                const float vv = floorf((dv + K.cy) + 0.5f);
+                in[q] = vz & (uu >= 0.0f) & (uu < (float)W) & (vv >= 0.0f) & (vv < (float)H);
+                fu[q] = in[q] ? uu : 0.0f;
+                fv[q] = in[q] ? vv : 0.0f;
+                j[q] = (int)__umul24((unsigned)(int)fv[q], (unsigned)W) + (int)fu[q];
+            }
+            f4v t[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                t[q] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rrec, j[q] * 16,
+                                                                                     0, 0));
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float tz = t[q].x;
+                const float tx = bp_div<kFast>((fu[q] - K.cx) * tz, K.fx, F.rfx);
+                const float ty = bp_div<kFast>((fv[q] - K.cy) * tz, K.fy, F.rfy);
+                const float dx = qx[q] - tx, dy = qy[q] - ty, dz = qz[q] - tz;
+                const float d2 = (dx * dx + dy * dy) + dz * dz;
+                const bool ok = in[q] & (tz > 0.0f) & (d2 < thr2);
+                const float n0 = ok ? t[q].y : 0.0f, n1 = ok ? t[q].z : 0.0f,
+                            n2 = ok ? t[q].w : 0.0f;
+                const float r = (n0 * dx + n1 * dy) + n2 * dz;
+                float Jf[6];
+                Jf[0] = qy[q] * n2 - qz[q] * n1;
+                Jf[1] = qz[q] * n0 - qx[q] * n2;
+                Jf[2] = qx[q] * n1 - qy[q] * n0;
+                Jf[3] = n0;
+                Jf[4] = n1;
+                Jf[5] = n2;
+                int kk = 0;
+#pragma unroll
+                for (int a = 0; a < 6; ++a)
+#pragma unroll
+                    for (int bb = a; bb < 6; ++bb) {
+                        acc[kk] = fma((double)Jf[a], (double)Jf[bb], acc[kk]);
+                        ++kk;
+                    }
+#pragma unroll
+                for (int a = 0; a < 6; ++a) acc[21 + a] = fma((double)Jf[a], (double)r, acc[21 + a]);
+                acc[27] = fma((double)r, (double)r, acc[27]);
+                nmatch += ok ? 1 : 0;
+            }
+        }
+        acc[28] = (double)nmatch;
+        COOP_MARK(k, 1);
+        {
+            double tot;
+            wave_reduce_scatter(acc, lane, tot);
+            if (!(lane & 1) && (lane >> 1) < kNeq) red[wave][lane >> 1] = tot;
+        }
+        __syncthreads();
+        double* part = partials + (size_t)(k & 1) * cs.n_pairs * G * kPartStride +
+                       (size_t)p * G * kPartStride;
+        COOP_MARK(k, 2);
+        if (wave == 0) {
+            // ---- publish this chunk's partial (sc1, drained), then arrive
+            double sum = 0.0;
+            if (lane < kPartStride) {
+                if (lane < kNeq)
+#pragma unroll
+                    for (int w = 0; w < kRedThreads / 64; ++w) sum += red[w][lane];
+                st_u64_sc1(part + (size_t)c * kPartStride + lane,
+                           (unsigned long long)__double_as_longlong(sum));
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0)
+                __hip_atomic_fetch_add(cnt + my_shard * kCoopShardStride, 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            COOP_MARK(k, 3);
+            // ---- wait for every workgroup of the pair: lanes 0..7 poll a shard each
+            const unsigned want = (unsigned)(k + 1) * n_s;
+            unsigned spins = 0;
+            int stop = 0;
+            for (;;) {
+                const unsigned have =
+                    lane < kCoopShards ? ld_u32_sc1(cnt + lane * kCoopShardStride) : 0u;
+                const bool done = __ballot(lane < kCoopShards && have < want) == 0ull;
+                if (done) break;
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > kCoopSpinMax || ld_u32_sc1(err) != 0u) {
+                    if (lane == 0)
+                        __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    stop = 1;
+                    break;
+                }
+            }
+            if (lane == 0) sh_stop = stop;
+            COOP_MARK(k, 4);
+        }
+        __syncthreads();
+        COOP_MARK(k, 5);
+        if (__builtin_amdgcn_readfirstlane(sh_stop)) {
+            timeout = true;
+            break;
+        }
+        // ---- every workgroup sums the pair's partials in k_icp's fixed order
+        {
+            const __amdgpu_buffer_rsrc_t rpart = __builtin_amdgcn_make_buffer_rsrc(
+                part, (short)0, G * kPartStride * (int)sizeof(double), 0x00020000);
+            const int t = threadIdx.x;
+            const int jc = t / kPieces, q = t - jc * kPieces;
+            if (jc < kSumCols) {
+                double s0 = 0.0, s1 = 0.0;
+                for (int bb = jc; bb < G; bb += 16 * kSumCols) {
+                    u4v v[16];
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int b = bb + i * kSumCols;
+                        v[i] = b < G ? __builtin_bit_cast(
+                                           u4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                                    rpart, (b * kPartStride + 2 * q) * 8, 0, 16))
+                                     : u4v{0u, 0u, 0u, 0u};
+                    }
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        s0 += __hiloint2double((int)v[i].y, (int)v[i].x);
+                        s1 += __hiloint2double((int)v[i].w, (int)v[i].z);
+                    }
+                }
+                colsum[jc][2 * q] = s0;
+                colsum[jc][2 * q + 1] = s1;
+            }
+        }
+        __syncthreads();
+        COOP_MARK(k, 6);
+        if (wave == 0) {
+            double tsum = 0.0;
+            if (lane < kNeq)
+#pragma unroll
+                for (int jj = 0; jj < kSumCols; ++jj) tsum += colsum[jj][lane];
+            double neq[kNeq];
+#pragma unroll
+            for (int qq = 0; qq < kNeq; ++qq) neq[qq] = readlane64(tsum, qq);
+            if (lane == 0) {
+                double Tm[16];
+#pragma unroll
+                for (int qq = 0; qq < 12; ++qq) Tm[qq] = sh_T64[qq];
+                if (c == 0 && cs.stats) {
+                    cs.stats[((size_t)p * cs.iters + k) * 2 + 0] = neq[28];
+                    cs.stats[((size_t)p * cs.iters + k) * 2 + 1] = neq[27];
+                }
+                double xi[6];
+                const int st = solve6(neq, xi);
+                if (st == 0) se3_exp_left(xi, Tm);
+                st_acc |= st;
+#pragma unroll
+                for (int qq = 0; qq < 12; ++qq) {
+                    sh_T64[qq] = Tm[qq];
+                    sh_T[qq] = (float)Tm[qq];
+                }
+            }
+        }
+        __syncthreads();
+        COOP_MARK(k, 7);
+    }
+
+    // ---- pair p's results, from its chunk-0 workgroup (replaces k_finish)
+    if (c == 0 && threadIdx.x < 16) {
+        const int i = threadIdx.x;
+        const double v = i < 12 ? sh_T64[i]
+                                : (cs.T_init ? cs.T_init[(size_t)p * 16 + i] : (i == 15 ? 1.0 : 0.0));
+        cs.T64[(size_t)p * 16 + i] = v;
+        if (i < 12) cs.T32[(size_t)p * 12 + i] = (float)v;
+        if (cs.T_out) cs.T_out[(size_t)p * 16 + i] = i < 12 ? (float)v : (i == 15 ? 1.0f : 0.0f);
+        if (i == 0) cs.status[p] = st_acc | (timeout ? YOUTH_STATUS_TIMEOUT : 0);
     }
 }
 
@@ -1245,6 +1641,14 @@ struct youth_icp_ctx {
     bool persistent = true;          // one k_icp launch per align (else per-iteration k_reduce)
     int icp_blocks_per_cu[4] = {0, 0, 0, 0};  // occupancy of k_icp<fast, aligned>
     int n_cu = 0;
+    // small batches: k_icp_coop (youth_icp_create reads the knobs)
+    bool coop = true;                // YOUTH_ICP_NO_COOP=1 disables
+    int coop_steps = 2;              // YOUTH_ICP_COOP_STEPS: min 1024-px steps per workgroup
+    int coop_max_pairs = 4;          // YOUTH_ICP_COOP_MAX_PAIRS (<= kCoopMaxPairs)
+    int coop_bpc[4][kCoopMaxSteps] = {};  // occupancy of k_icp_coop<fast, aligned, steps>
+    unsigned* d_coop = nullptr;      // 2 counter sets of kCoopSetWords
+    int coop_par = 0;                // set used by the next coop call
+    int last_coop_G = 0, last_coop_steps = 0;
 
     int last_pairs = 0;
     int last_iters = 0;
@@ -1434,10 +1838,85 @@ static int launch_reduce(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, P
     return ev_end(c, s, &ep);
 }
 
-static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, PairMap pm,
-                          int n_pairs, const double* T_init_host)
+// Small-batch plan: the fewest 1024-px steps per workgroup (>= coop_steps)
+// whose n_pairs x G workgroups fit the co-resident capacity with one block
+// per CU to spare (cooperative launch admission, MI355X_MICROARCH.md).
+static bool coop_plan(const youth_icp_ctx* c, int n_pairs, int var, int* steps_out, int* G_out)
+{
+    if (!c->coop || n_pairs > c->coop_max_pairs || n_pairs > kCoopMaxPairs) return false;
+    for (int st = c->coop_steps; st <= kCoopMaxSteps; ++st) {
+        const int chunk = st * kRedStep;
+        const int G = (c->N + chunk - 1) / chunk;
+        const long long cap = (long long)c->n_cu * (c->coop_bpc[var][st - 1] - 1);
+        if ((long long)G * n_pairs <= cap) {
+            *steps_out = st;
+            *G_out = G;
+            return true;
+        }
+    }
+    return false;
+}
+
+template <bool kFast, bool kAligned>
+static const void* coop_kernel(int steps)
+{
+    switch (steps) {
+    case 1: return (const void*)k_icp_coop<kFast, kAligned, 1>;
+    case 2: return (const void*)k_icp_coop<kFast, kAligned, 2>;
+    case 3: return (const void*)k_icp_coop<kFast, kAligned, 3>;
+    default: return (const void*)k_icp_coop<kFast, kAligned, 4>;
+    }
+}
+
+static const void* coop_kernel(int var, int steps)
+{
+    switch (var) {
+    case 0: return coop_kernel<false, false>(steps);
+    case 1: return coop_kernel<false, true>(steps);
+    case 2: return coop_kernel<true, false>(steps);
+    default: return coop_kernel<true, true>(steps);
+    }
+}
+
+static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, PairMap pm,
+                       int n_pairs, const double* dTi, float* d_T_out, int var, int steps, int G)
 {
     const int iters = c->prm.iters;
+    int rc = ensure_partials(c, (size_t)2 * n_pairs * G * kPartStride);
+    if (rc) return rc;
+    unsigned* set = c->d_coop + (size_t)c->coop_par * kCoopSetWords;
+    unsigned* set_next = c->d_coop + (size_t)(c->coop_par ^ 1) * kCoopSetWords;
+    c->coop_par ^= 1;
+    CoopState cs{dTi, c->d_T64, c->d_T32, c->d_status, c->d_stats, d_T_out,
+                 set, set_next, c->d_head, iters, n_pairs, G, steps * kRedStep};
+    const float4* recs = c->d_rec;
+    size_t P = c->P;
+    int W = c->W, H = c->H;
+    Intr K = c->K;
+    FastK F = c->F;
+    float thr2 = c->prm.dist_thresh * c->prm.dist_thresh;
+    double* partials = c->d_partials;
+    void* args[] = {(void*)&dsrc, (void*)&recs, (void*)&P, (void*)&pm, (void*)&W, (void*)&H,
+                    (void*)&K, (void*)&F, (void*)&thr2, (void*)&partials, (void*)&cs};
+    EventPair ep{};
+    rc = ev_begin(c, s, &ep, 0);
+    if (rc) return rc;
+    HIP_TRY(hipLaunchCooperativeKernel(coop_kernel(var, steps), dim3((unsigned)(n_pairs * G)),
+                                       dim3(kRedThreads), args, 0, s));
+    c->last_coop_G = G;
+    c->last_coop_steps = steps;
+    return ev_end(c, s, &ep);
+}
+
+// All ICP iterations of n_pairs pairs.  *exported is set when the kernel
+// also wrote the fp32 4x4 poses to d_T_out (k_icp_coop); otherwise the
+// caller runs export_poses.
+static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, PairMap pm,
+                          int n_pairs, const double* T_init_host, float* d_T_out = nullptr,
+                          bool* exported = nullptr)
+{
+    const int iters = c->prm.iters;
+    if (exported) *exported = false;
     int rc = ensure_stats(c, iters > 0 ? iters : 1);
     if (rc) return rc;
     const double* dTi = nullptr;
@@ -1445,6 +1924,20 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
         HIP_TRY(hipMemcpyAsync(c->d_Tinit, T_init_host, (size_t)n_pairs * 16 * sizeof(double),
                                hipMemcpyHostToDevice, s));
         dTi = c->d_Tinit;
+    }
+    {
+        const bool aligned = (reinterpret_cast<uintptr_t>(dsrc) % 8 == 0) && (c->W % 4 == 0);
+        const int var = (c->fast ? 2 : 0) | (aligned ? 1 : 0);
+        int steps = 0, G = 0;
+        if (iters > 0 && coop_plan(c, n_pairs, var, &steps, &G)) {
+            rc = launch_coop(c, s, dsrc, pm, n_pairs, dTi, d_T_out, var, steps, G);
+            if (rc) return rc;
+            if (exported) *exported = d_T_out != nullptr;
+            c->last_pairs = n_pairs;
+            c->last_iters = iters;
+            c->last_stream = s;
+            return YOUTH_OK;
+        }
     }
     const bool persistent = c->persistent && iters > 0;
     hipLaunchKernelGGL(k_init, dim3((n_pairs + 63) / 64), dim3(64), 0, s, dTi, n_pairs, c->d_T64,
@@ -1571,7 +2064,8 @@ void youth_icp_destroy(youth_icp_ctx* c)
         }
     void* bufs[] = {c->d_depth, c->d_rec,   c->d_xyz,      c->d_T64, c->d_T32,   c->d_status,
                     c->d_Tinit, c->d_stats, c->d_partials, c->d_neq, c->d_assoc, c->d_Tout,
-                    c->d_flag,  c->d_arrivals, c->d_arr_it, c->d_epoch, c->d_head};
+                    c->d_flag,  c->d_arrivals, c->d_arr_it, c->d_epoch, c->d_head,
+                    c->d_coop};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1656,7 +2150,26 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         }
         const char* np = getenv("YOUTH_ICP_NO_PERSISTENT");
         c->persistent = !(np && *np && *np != '0');
+        for (int v = 0; v < 4; ++v)
+            for (int st = 1; st <= kCoopMaxSteps; ++st) {
+                int nb = 0;
+                if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, coop_kernel(v, st),
+                                                                      kRedThreads, 0)) !=
+                    hipSuccess)
+                    return fail("occupancy coop", e);
+                c->coop_bpc[v][st - 1] = nb;
+            }
+        const char* nc = getenv("YOUTH_ICP_NO_COOP");
+        c->coop = !(nc && *nc && *nc != '0');
+        const char* cst = getenv("YOUTH_ICP_COOP_STEPS");
+        if (cst && atoi(cst) >= 1 && atoi(cst) <= kCoopMaxSteps) c->coop_steps = atoi(cst);
+        const char* cmp = getenv("YOUTH_ICP_COOP_MAX_PAIRS");
+        if (cmp && atoi(cmp) >= 0) c->coop_max_pairs = atoi(cmp);
     }
+    if ((e = hipMalloc(&c->d_coop, 2 * kCoopSetWords * sizeof(unsigned))) != hipSuccess)
+        return fail("hipMalloc coop", e);
+    if ((e = hipMemset(c->d_coop, 0, 2 * kCoopSetWords * sizeof(unsigned))) != hipSuccess)
+        return fail("memset coop", e);
     const size_t arr_bytes = (MF * sizeof(unsigned) + 15) / 16 * 16;
     if ((e = hipMalloc(&c->d_arrivals, arr_bytes)) != hipSuccess)
         return fail("hipMalloc arrivals", e);
@@ -1683,9 +2196,10 @@ int youth_icp_align_pairs_device(youth_icp_ctx* c, const int16_t* d_src, const i
     // targets -> records [0, n); sources are read from d_src by k_reduce
     rc = launch_prep(c, s, d_dst, n_pairs, 0, false);
     if (rc) return rc;
-    rc = run_iterations(c, s, d_src, PairMap{0, 0}, n_pairs, T_init);
+    bool exported = false;
+    rc = run_iterations(c, s, d_src, PairMap{0, 0}, n_pairs, T_init, d_T_out, &exported);
     if (rc) return rc;
-    return export_poses(c, s, n_pairs, d_T_out);
+    return exported ? YOUTH_OK : export_poses(c, s, n_pairs, d_T_out);
 }
 
 int youth_icp_align_sequence_device(youth_icp_ctx* c, const int16_t* d_frames, int n_frames,
@@ -1700,9 +2214,10 @@ int youth_icp_align_sequence_device(youth_icp_ctx* c, const int16_t* d_frames, i
     rc = launch_prep(c, s, d_frames, n_frames - 1, 0, false);
     if (rc) return rc;
     // pair k: source depth frame k+1, target record frame k
-    rc = run_iterations(c, s, d_frames, PairMap{1, 0}, n_frames - 1, nullptr);
+    bool exported = false;
+    rc = run_iterations(c, s, d_frames, PairMap{1, 0}, n_frames - 1, nullptr, d_T_out, &exported);
     if (rc) return rc;
-    return export_poses(c, s, n_frames - 1, d_T_out);
+    return exported ? YOUTH_OK : export_poses(c, s, n_frames - 1, d_T_out);
 }
 
 int youth_icp_sync(youth_icp_ctx* c, void* stream)

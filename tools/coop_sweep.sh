@@ -1,0 +1,22 @@
+#!/bin/bash
+# Small-batch A/B on the GPU box: k_icp_coop (steps 2..4) vs the persistent
+# k_icp (YOUTH_ICP_NO_COOP=1), pairs 1/2/4, interleaved in one process tree.
+# Usage: tools/coop_sweep.sh [rounds]
+set -uo pipefail
+R=${1:-2}
+one() {  # label env... -- bench args
+    local label=$1; shift
+    local envs=(); while [ "$1" != "--" ]; do envs+=("$1"); shift; done; shift
+    local out
+    out=$(env "${envs[@]}" timeout -k 10 120 python3 bench.py --no-cpu-baseline --no-host-io "$@") || { echo "$label FAILED"; return 1; }
+    python3 -c "import json,sys; d=json.loads(sys.argv[1]); k=d['kernel_ms_per_step']; print(f\"{sys.argv[2]:34s} {d['value']:9.0f} aligns/s  ms/step {d['ms_per_step']*1e3:7.1f} us  icp {k['k_reduce']*1e3:7.1f} us  prep {k['k_prep']*1e3:5.1f} us\")" "$out" "$label"
+}
+for r in $(seq 1 $R); do
+  for np in 1 2 4; do
+    S=$((200 / np + 20))
+    one "pairs=$np persistent" YOUTH_ICP_NO_COOP=1 -- --pairs-per-gpu $np --steps $S --warmup 20 || exit 1
+    for st in 2 3 4; do
+      one "pairs=$np coop steps=$st" YOUTH_ICP_COOP_STEPS=$st YOUTH_ICP_COOP_MAX_PAIRS=16 -- --pairs-per-gpu $np --steps $S --warmup 20 || exit 1
+    done
+  done
+done
