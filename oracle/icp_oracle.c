@@ -211,10 +211,21 @@ void oracle_se3_exp(const double xi[6], double E[16])
     const double wx = xi[0], wy = xi[1], wz = xi[2];
     const double th2 = (wx * wx + wy * wy) + wz * wz;
     double a, b, c;
-    if (th2 < 1e-10) {
-        a = 1.0 - th2 / 6.0;
-        b = 0.5 - th2 / 24.0;
-        c = 1.0 / 6.0 - th2 / 120.0;
+    if (th2 < 0x1p-7) {
+        /* a = sin(t)/t, b = (1 - cos t)/t^2, c = (t - sin t)/t^3 as degree-5
+         * Taylor polynomials in x = t^2 (t < 5 deg, truncation < 1e-22),
+         * Horner with explicit fma: the same correctly rounded operations
+         * on the GPU (se3_exp_left), so both agree bit for bit */
+        const double x = th2;
+        a = fma(x, fma(x, fma(x, fma(x, fma(x, -0x1.ae64567f544e4p-26, 0x1.71de3a556c734p-19),
+                                        -0x1.a01a01a01a01ap-13), 0x1.1111111111111p-7),
+                       -0x1.5555555555555p-3), 0x1.0000000000000p+0);
+        b = fma(x, fma(x, fma(x, fma(x, fma(x, -0x1.1eed8eff8d898p-29, 0x1.27e4fb7789f5cp-22),
+                                        -0x1.a01a01a01a01ap-16), 0x1.6c16c16c16c17p-10),
+                       -0x1.5555555555555p-5), 0x1.0000000000000p-1);
+        c = fma(x, fma(x, fma(x, fma(x, fma(x, -0x1.6124613a86d09p-33, 0x1.ae64567f544e4p-26),
+                                        -0x1.71de3a556c734p-19), 0x1.a01a01a01a01ap-13),
+                       -0x1.1111111111111p-7), 0x1.5555555555555p-3);
     } else {
         const double th = sqrt(th2);
         const double s = sin(th), co = cos(th);

@@ -488,10 +488,17 @@ __device__ void se3_exp_left(const double xi[6], double* T)
     const double wx = xi[0], wy = xi[1], wz = xi[2];
     const double th2 = (wx * wx + wy * wy) + wz * wz;
     double a, b, c;
-    if (th2 < 1e-10) {
-        a = 1.0 - th2 / 6.0;
-        b = 0.5 - th2 / 24.0;
-        c = 1.0 / 6.0 - th2 / 120.0;
+    if (th2 < 0x1p-7) {  // spec a10: Taylor in th2 (oracle_se3_exp: same fma chain)
+        const double x = th2;
+        a = fma(x, fma(x, fma(x, fma(x, fma(x, -0x1.ae64567f544e4p-26, 0x1.71de3a556c734p-19),
+                                        -0x1.a01a01a01a01ap-13), 0x1.1111111111111p-7),
+                       -0x1.5555555555555p-3), 0x1.0000000000000p+0);
+        b = fma(x, fma(x, fma(x, fma(x, fma(x, -0x1.1eed8eff8d898p-29, 0x1.27e4fb7789f5cp-22),
+                                        -0x1.a01a01a01a01ap-16), 0x1.6c16c16c16c17p-10),
+                       -0x1.5555555555555p-5), 0x1.0000000000000p-1);
+        c = fma(x, fma(x, fma(x, fma(x, fma(x, -0x1.6124613a86d09p-33, 0x1.ae64567f544e4p-26),
+                                        -0x1.71de3a556c734p-19), 0x1.a01a01a01a01ap-13),
+                       -0x1.1111111111111p-7), 0x1.5555555555555p-3);
     } else {
         const double th = sqrt(th2);
         double s, co;
@@ -973,6 +980,66 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce(
     }
 }
 
+// Fixed-order sum of a pair's nblk partial rows (kPartStride doubles each,
+// written with sc1 stores by other workgroups, read with sc1 loads only).
+// Called by every thread of the workgroup.  Thread (column j, piece q) with
+// j < kSumCols loads rows j, j + 16, ... in batches of 16 16-byte pieces and
+// adds each batch as a pairwise tree (depth 4), batches in order; then wave 0
+// lane l < kNeq adds the 16 column sums of value l as a pairwise tree.  The
+// tree keeps the dependent fp64 adds per value at ~8 + batches instead of the
+// 16 + rows of a running sum (the solve waits on it every iteration).  Returns
+// the pair total of value `lane` in wave 0's lanes < kNeq (0 elsewhere).
+template <int kN>
+__device__ __forceinline__ double tree_sum(const double* v)
+{
+    if constexpr (kN == 1) {
+        return v[0];
+    } else {
+        return tree_sum<kN / 2>(v) + tree_sum<kN / 2>(v + kN / 2);
+    }
+}
+
+__device__ __forceinline__ double sum_pair_rows(__amdgpu_buffer_rsrc_t rpart, int nblk,
+                                                double (*colsum)[kPartStride])
+{
+    const int t = threadIdx.x;
+    const int j = t / kPieces, q = t - j * kPieces;
+    if (j < kSumCols) {
+        double s0 = 0.0, s1 = 0.0;
+        for (int bb = j; bb < nblk; bb += 16 * kSumCols) {
+            u4v v[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int b = bb + i * kSumCols;
+                // aux 16 = sc1 (bypass this CU's L1: written by other CUs)
+                v[i] = b < nblk ? __builtin_bit_cast(
+                                      u4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                               rpart, (b * kPartStride + 2 * q) * 8, 0, 16))
+                                : u4v{0u, 0u, 0u, 0u};
+            }
+            double a0[16], a1[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                a0[i] = __hiloint2double((int)v[i].y, (int)v[i].x);
+                a1[i] = __hiloint2double((int)v[i].w, (int)v[i].z);
+            }
+            s0 += tree_sum<16>(a0);
+            s1 += tree_sum<16>(a1);
+        }
+        colsum[j][2 * q] = s0;
+        colsum[j][2 * q + 1] = s1;
+    }
+    __syncthreads();
+    double tsum = 0.0;
+    if (t < kNeq) {
+        double c[kSumCols];
+#pragma unroll
+        for (int jj = 0; jj < kSumCols; ++jj) c[jj] = colsum[jj][t];
+        tsum = tree_sum<kSumCols>(c);
+    }
+    return tsum;
+}
+
 // ------------------------------------------------------------------- k_icp --
 // ONE persistent launch for all `iters` iterations of a batch.
 //
@@ -1150,47 +1217,17 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
         __syncthreads();
         if (__builtin_amdgcn_readfirstlane(sh_last)) {
             // ---- last arriver of (p, k): every wave sums a share of the
-            // pair's partials (sc1 16-byte loads, one batch for <= 256
-            // chunks): thread (col j, piece q) adds rows j, j + 16, ... in
-            // order; then wave 0 adds the 16 column sums in order, solves,
-            // publishes the pose, then the epoch.
+            // pair's partials (sum_pair_rows: sc1 16-byte loads, one batch
+            // for <= 256 chunks, fixed tree order); wave 0 solves, publishes
+            // the pose, then the epoch.
             const __amdgpu_buffer_rsrc_t rpart = __builtin_amdgcn_make_buffer_rsrc(
                 partials + (size_t)p * is.nblk * kPartStride, (short)0,
                 is.nblk * kPartStride * (int)sizeof(double), 0x00020000);
-            const int t = threadIdx.x;
-            const int j = t / kPieces, q = t - j * kPieces;
-            if (j < kSumCols) {
-                double s0 = 0.0, s1 = 0.0;
-                for (int bb = j; bb < is.nblk; bb += 16 * kSumCols) {
-                    u4v v[16];
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const int b = bb + i * kSumCols;
-                        // aux 16 = sc1 (bypass this CU's L1: written by other CUs)
-                        v[i] = b < is.nblk ? __builtin_bit_cast(
-                                                 u4v, __builtin_amdgcn_raw_buffer_load_b128(
-                                                          rpart, (b * kPartStride + 2 * q) * 8, 0,
-                                                          16))
-                                           : u4v{0u, 0u, 0u, 0u};
-                    }
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        s0 += __hiloint2double((int)v[i].y, (int)v[i].x);
-                        s1 += __hiloint2double((int)v[i].w, (int)v[i].z);
-                    }
-                }
-                colsum[j][2 * q] = s0;
-                colsum[j][2 * q + 1] = s1;
-            } else if (t >= kSumCols * kPieces && t < kSumCols * kPieces + 12) {
-                sh_T64[t - kSumCols * kPieces] = __longlong_as_double((long long)ld_u64_sc1(
-                    is.T64 + (size_t)p * 16 + (t - kSumCols * kPieces)));
-            }
-            __syncthreads();
+            if (threadIdx.x >= 64 && threadIdx.x < 64 + 12)
+                sh_T64[threadIdx.x - 64] = __longlong_as_double(
+                    (long long)ld_u64_sc1(is.T64 + (size_t)p * 16 + (threadIdx.x - 64)));
+            const double tsum = sum_pair_rows(rpart, is.nblk, colsum);
             if (wave == 0) {
-                double tsum = 0.0;
-                if (lane < kNeq)
-#pragma unroll
-                    for (int jj = 0; jj < kSumCols; ++jj) tsum += colsum[jj][lane];
                 double neq[kNeq];
 #pragma unroll
                 for (int qq = 0; qq < kNeq; ++qq) neq[qq] = readlane64(tsum, qq);
@@ -1239,9 +1276,9 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
 //   * ONE cooperative launch of n_pairs x G co-resident workgroups replaces
 //     k_init + k_icp + k_finish; workgroup b owns chunk c = b % G of pair
 //     p = b / G for every iteration (no queue);
-//   * its source pixels (kSteps x 1024) are loaded and back-projected ONCE
-//     and stay in registers; its record gathers hit the same lines every
-//     iteration (L1/L2-warm);
+//   * its source pixels (npx per lane) are loaded and back-projected ONCE
+//     into LDS; its record gathers hit the same lines every iteration
+//     (L1/L2-warm);
 //   * per iteration ONE hand-off: each workgroup publishes its partial
 //     (sc1 stores, drained) and adds to one of 8 arrival counters of its pair
 //     (shard = c & 7, one 128-B line each); every workgroup polls the 8
@@ -1258,7 +1295,7 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
 // every spin is still bounded (timeout -> YOUTH_STATUS_TIMEOUT, no hang).
 constexpr int kCoopShards = 8;
 constexpr int kCoopShardStride = 32;  // words: one 128-B line per shard
-constexpr int kCoopMaxSteps = 4;
+constexpr int kCoopMaxPx = 32;       // source pixels per lane (LDS: 3 x 32 KB)
 constexpr int kCoopMaxPairs = 16;     // counter words per set: 16 x 8 x 32
 constexpr int kCoopSetWords = kCoopMaxPairs * kCoopShards * kCoopShardStride + kCoopShardStride;
 constexpr unsigned kCoopSpinMax = 1u << 22;  // polls (~1 us each): seconds, never reached
@@ -1273,35 +1310,130 @@ struct CoopState {
     unsigned* set;         // this call's counters [pair][shard * 32] + timeout word
     unsigned* set_next;    // the next call's: zeroed here
     unsigned* head_err;    // k_icp's queue words: error/telemetry cleared for get_poses
-    int iters, n_pairs, G, chunk;
+    int iters, n_pairs, G, npx;  // G workgroups per pair, npx source pixels per lane
 };
 
 // Phase timestamps for tools/coopbench only (never in the product build):
 // thread 0 of every workgroup records s_memrealtime (100 MHz) at 8 points of
-// each iteration into coop_phase[block][iteration][8].
+// each iteration into coop_phase[block][iteration][16] (slots 8-10: solve).
 #ifdef YOUTH_COOP_PHASES
 __device__ unsigned long long* coop_phase;
 #define COOP_MARK(k, slot)                                                           \
     do {                                                                             \
         if (threadIdx.x == 0 && coop_phase && (k) < 32)                              \
-            coop_phase[((size_t)blockIdx.x * 32 + (k)) * 8 + (slot)] =               \
+            coop_phase[((size_t)blockIdx.x * 32 + (k)) * 16 + (slot)] =              \
+                __builtin_amdgcn_s_memrealtime();                                    \
+    } while (0)
+#define COOP_MARK_WAVE(k, slot)                                                      \
+    do {                                                                             \
+        if ((threadIdx.x & 63) == 0 && threadIdx.x && coop_phase && (k) < 32)       \
+            coop_phase[((size_t)blockIdx.x * 32 + (k)) * 16 + (slot)] =              \
                 __builtin_amdgcn_s_memrealtime();                                    \
     } while (0)
 #else
 #define COOP_MARK(k, slot) \
     do {                   \
     } while (0)
+#define COOP_MARK_WAVE(k, slot) \
+    do {                        \
+    } while (0)
 #endif
 
-template <bool kFast, bool kAligned, int kSteps>
-__global__ __launch_bounds__(kRedThreads, 2) void k_icp_coop(const int16_t* __restrict__ dsrc,
+// Spec a7-a9 for Q source pixels already back-projected (px = pixel slots
+// s0 .. s0+Q-1 of this lane in the LDS planes X/Y/Z [slot][256]): transform,
+// project, Q record gathers back to back, residual, Jacobian, exact products
+// into the fp64 accumulators.  Same expressions as accumulate_chunk.
+template <bool kFast, int Q, int kThreads>
+__device__ __forceinline__ void coop_group(const float* __restrict__ X, const float* __restrict__ Y,
+                                           const float* __restrict__ Z, int s0, const float* T,
+                                           __amdgpu_buffer_rsrc_t rrec, int W, int H,
+                                           const Intr& K, const FastK& F, float thr2,
+                                           double* acc, int& nmatch)
+{
+    const int t = threadIdx.x;
+    float qx[Q], qy[Q], qz[Q], fu[Q], fv[Q];
+    bool in[Q];
+    int j[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const float sx = X[(s0 + q) * kThreads + t];
+        const float sy = Y[(s0 + q) * kThreads + t];
+        const float sz = Z[(s0 + q) * kThreads + t];
+        qx[q] = ((T[0] * sx + T[1] * sy) + T[2] * sz) + T[3];
+        qy[q] = ((T[4] * sx + T[5] * sy) + T[6] * sz) + T[7];
+        qz[q] = ((T[8] * sx + T[9] * sy) + T[10] * sz) + T[11];
+        const bool vz = (sz > 0.0f) & (qz[q] > 0.0f);
+        const float qzs = vz ? qz[q] : 1.0f;
+        const float nu = K.fx * qx[q], nv = K.fy * qy[q];
+        float du, dv;
+        if (proj_den_ok(qzs)) {
+            const float r = proj_recip(qzs);
+            du = proj_div_one(nu, qzs, r);
+            dv = proj_div_one(nv, qzs, r);
+        } else {
+            du = nu / qzs;
+            dv = nv / qzs;
+        }
+        const float uu = floorf((du + K.cx) + 0.5f);
+        const float vv = floorf((dv + K.cy) + 0.5f);
+        in[q] = vz & (uu >= 0.0f) & (uu < (float)W) & (vv >= 0.0f) & (vv < (float)H);
+        fu[q] = in[q] ? uu : 0.0f;
+        fv[q] = in[q] ? vv : 0.0f;
+        j[q] = (int)__umul24((unsigned)(int)fv[q], (unsigned)W) + (int)fu[q];
+    }
+    f4v rec[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+        rec[q] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rrec, j[q] * 16, 0, 0));
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const float tz = rec[q].x;
+        const float tx = bp_div<kFast>((fu[q] - K.cx) * tz, K.fx, F.rfx);
+        const float ty = bp_div<kFast>((fv[q] - K.cy) * tz, K.fy, F.rfy);
+        const float dx = qx[q] - tx, dy = qy[q] - ty, dz = qz[q] - tz;
+        const float d2 = (dx * dx + dy * dy) + dz * dz;
+        const bool ok = in[q] & (tz > 0.0f) & (d2 < thr2);
+        const float n0 = ok ? rec[q].y : 0.0f, n1 = ok ? rec[q].z : 0.0f, n2 = ok ? rec[q].w : 0.0f;
+        const float r = (n0 * dx + n1 * dy) + n2 * dz;
+        float Jf[6];
+        Jf[0] = qy[q] * n2 - qz[q] * n1;
+        Jf[1] = qz[q] * n0 - qx[q] * n2;
+        Jf[2] = qx[q] * n1 - qy[q] * n0;
+        Jf[3] = n0;
+        Jf[4] = n1;
+        Jf[5] = n2;
+        int kk = 0;
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+            for (int bb = a; bb < 6; ++bb) {
+                acc[kk] = fma((double)Jf[a], (double)Jf[bb], acc[kk]);
+                ++kk;
+            }
+#pragma unroll
+        for (int a = 0; a < 6; ++a) acc[21 + a] = fma((double)Jf[a], (double)r, acc[21 + a]);
+        acc[27] = fma((double)r, (double)r, acc[27]);
+        nmatch += ok ? 1 : 0;
+    }
+}
+
+// Pixels per lane cs.npx is a launch parameter: the host picks it so the
+// n_pairs x G workgroups spread over every CU (the pixel phase of one wave
+// is latency-bound, so it costs ~npx x the per-pixel chain: DESIGN.md §5);
+// kThreads = 512 puts two waves on each SIMD to hide that latency.  Lane t
+// of chunk c owns source pixels c kThreads npx + s kThreads + t, s < npx;
+// their back-projected X/Y/Z live in dynamic LDS [3][npx][kThreads] for the
+// whole launch.
+template <bool kFast, int kThreads>
+__global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restrict__ dsrc,
                                                              const float4* __restrict__ recs,
                                                              size_t P, PairMap pm, int W, int H,
                                                              Intr K, FastK F, float thr2,
                                                              double* __restrict__ partials,
                                                              CoopState cs)
 {
-    __shared__ double red[kRedThreads / 64][kNeq];
+    extern __shared__ float coop_src[];  // [3][npx][kThreads]
+    __shared__ double red[kThreads / 64][kNeq];
     __shared__ double colsum[kSumCols][kPartStride];
     __shared__ double sh_T64[12];
     __shared__ float sh_T[12];
@@ -1309,14 +1441,18 @@ __global__ __launch_bounds__(kRedThreads, 2) void k_icp_coop(const int16_t* __re
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int G = cs.G;
+    const int npx = cs.npx;
     const int p = blockIdx.x / G;
     const int c = blockIdx.x - p * G;
     const int N = W * H;
     unsigned* cnt = cs.set + (size_t)p * kCoopShards * kCoopShardStride;
     unsigned* err = cs.set + (size_t)kCoopMaxPairs * kCoopShards * kCoopShardStride;
+    float* X = coop_src;
+    float* Y = coop_src + npx * kThreads;
+    float* Z = coop_src + 2 * npx * kThreads;
 
     if (blockIdx.x == 0) {
-        for (int i = threadIdx.x; i < kCoopSetWords; i += kRedThreads) st_u32_sc1(cs.set_next + i, 0u);
+        for (int i = threadIdx.x; i < kCoopSetWords; i += kThreads) st_u32_sc1(cs.set_next + i, 0u);
         if (threadIdx.x == 0) {
             st_u32_sc1(cs.head_err + kQError, 0u);
             st_u32_sc1(cs.head_err + kQSpins, 0u);
@@ -1329,29 +1465,20 @@ __global__ __launch_bounds__(kRedThreads, 2) void k_icp_coop(const int16_t* __re
         sh_T64[threadIdx.x] = v;
         sh_T[threadIdx.x] = (float)v;
     }
-
     // ---- this workgroup's source pixels, back-projected once (spec a2)
-    const int16_t* sD = dsrc + (size_t)(pm.src0 + p) * N;
-    const int base = c * cs.chunk;
-    float sx[kSteps][4], sy[kSteps][4], sz[kSteps][4];
-#pragma unroll
-    for (int s = 0; s < kSteps; ++s) {
-        const int i = base + s * kRedStep + threadIdx.x * 4;
-        short4 d4 = make_short4(0, 0, 0, 0);
-        if (i < N) d4 = load_depth4<kAligned>(sD, i, N);
-        const int dd[4] = {d4.x, d4.y, d4.z, d4.w};
-        const int ii = i < N ? i : 0;
-        const int v0 = ii / W;
-        const int u0 = ii - v0 * W;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            int u = u0 + q, v = v0;
-            if (!kAligned) {
-                const bool wrap = u >= W;
-                u = wrap ? u - W : u;
-                v = wrap ? v + 1 : v;
-            }
-            backproject<kFast>((i + q) < N ? dd[q] : 0, u, v, K, F, sx[s][q], sy[s][q], sz[s][q]);
+    {
+        const int16_t* sD = dsrc + (size_t)(pm.src0 + p) * N;
+        const int base = c * npx * kThreads + threadIdx.x;
+        for (int s = 0; s < npx; ++s) {
+            const int i = base + s * kThreads;
+            const int d = i < N ? (int)sD[i] : 0;
+            const int ii = i < N ? i : 0;
+            const int v = ii / W;
+            float x, y, z;
+            backproject<kFast>(d, ii - v * W, v, K, F, x, y, z);
+            X[s * kThreads + threadIdx.x] = x;
+            Y[s * kThreads + threadIdx.x] = y;
+            Z[s * kThreads + threadIdx.x] = z;
         }
     }
     const __amdgpu_buffer_rsrc_t rrec = __builtin_amdgcn_make_buffer_rsrc(
@@ -1375,78 +1502,22 @@ __global__ __launch_bounds__(kRedThreads, 2) void k_icp_coop(const int16_t* __re
 #pragma unroll
         for (int q = 0; q < kNeq; ++q) acc[q] = 0.0;
         int nmatch = 0;
-#pragma unroll
-        for (int s = 0; s < kSteps; ++s) {
-            float qx[4], qy[4], qz[4], fu[4], fv[4];
-            bool in[4];
-            int j[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                // spec a7 (same expressions as accumulate_chunk)
-                qx[q] = ((T[0] * sx[s][q] + T[1] * sy[s][q]) + T[2] * sz[s][q]) + T[3];
-                qy[q] = ((T[4] * sx[s][q] + T[5] * sy[s][q]) + T[6] * sz[s][q]) + T[7];
-                qz[q] = ((T[8] * sx[s][q] + T[9] * sy[s][q]) + T[10] * sz[s][q]) + T[11];
-                const bool vz = (sz[s][q] > 0.0f) & (qz[q] > 0.0f);
-                const float qzs = vz ? qz[q] : 1.0f;
-                const float nu = K.fx * qx[q], nv = K.fy * qy[q];
-                float du, dv;
-                if (proj_den_ok(qzs)) {
-                    const float r = proj_recip(qzs);
-                    du = proj_div_one(nu, qzs, r);
-                    dv = proj_div_one(nv, qzs, r);
-                } else {
-                    du = nu / qzs;
-                    dv = nv / qzs;
-                }
-                const float uu = floorf((du + K.cx) + 0.5f);
-                const float vv = floorf((dv + K.cy) + 0.5f);
-                in[q] = vz & (uu >= 0.0f) & (uu < (float)W) & (vv >= 0.0f) & (vv < (float)H);
-                fu[q] = in[q] ? uu : 0.0f;
-                fv[q] = in[q] ? vv : 0.0f;
-                j[q] = (int)__umul24((unsigned)(int)fv[q], (unsigned)W) + (int)fu[q];
-            }
-            f4v t[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                t[q] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rrec, j[q] * 16,
-                                                                                     0, 0));
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float tz = t[q].x;
-                const float tx = bp_div<kFast>((fu[q] - K.cx) * tz, K.fx, F.rfx);
-                const float ty = bp_div<kFast>((fv[q] - K.cy) * tz, K.fy, F.rfy);
-                const float dx = qx[q] - tx, dy = qy[q] - ty, dz = qz[q] - tz;
-                const float d2 = (dx * dx + dy * dy) + dz * dz;
-                const bool ok = in[q] & (tz > 0.0f) & (d2 < thr2);
-                const float n0 = ok ? t[q].y : 0.0f, n1 = ok ? t[q].z : 0.0f,
-                            n2 = ok ? t[q].w : 0.0f;
-                const float r = (n0 * dx + n1 * dy) + n2 * dz;
-                float Jf[6];
-                Jf[0] = qy[q] * n2 - qz[q] * n1;
-                Jf[1] = qz[q] * n0 - qx[q] * n2;
-                Jf[2] = qx[q] * n1 - qy[q] * n0;
-                Jf[3] = n0;
-                Jf[4] = n1;
-                Jf[5] = n2;
-                int kk = 0;
-#pragma unroll
-                for (int a = 0; a < 6; ++a)
-#pragma unroll
-                    for (int bb = a; bb < 6; ++bb) {
-                        acc[kk] = fma((double)Jf[a], (double)Jf[bb], acc[kk]);
-                        ++kk;
-                    }
-#pragma unroll
-                for (int a = 0; a < 6; ++a) acc[21 + a] = fma((double)Jf[a], (double)r, acc[21 + a]);
-                acc[27] = fma((double)r, (double)r, acc[27]);
-                nmatch += ok ? 1 : 0;
-            }
+        int s0 = 0;
+        for (; s0 + 4 <= npx; s0 += 4)
+            coop_group<kFast, 4, kThreads>(X, Y, Z, s0, T, rrec, W, H, K, F, thr2, acc, nmatch);
+        switch (npx - s0) {  // wave-uniform tail
+        case 3: coop_group<kFast, 3, kThreads>(X, Y, Z, s0, T, rrec, W, H, K, F, thr2, acc, nmatch); break;
+        case 2: coop_group<kFast, 2, kThreads>(X, Y, Z, s0, T, rrec, W, H, K, F, thr2, acc, nmatch); break;
+        case 1: coop_group<kFast, 1, kThreads>(X, Y, Z, s0, T, rrec, W, H, K, F, thr2, acc, nmatch); break;
+        default: break;
         }
         acc[28] = (double)nmatch;
         COOP_MARK(k, 1);
+        if (wave < 4) COOP_MARK_WAVE(k, 11 + wave);  // slots 12-14: waves 1-3 pixel loop done
         {
             double tot;
             wave_reduce_scatter(acc, lane, tot);
+            COOP_MARK(k, 11);
             if (!(lane & 1) && (lane >> 1) < kNeq) red[wave][lane >> 1] = tot;
         }
         __syncthreads();
@@ -1459,7 +1530,7 @@ __global__ __launch_bounds__(kRedThreads, 2) void k_icp_coop(const int16_t* __re
             if (lane < kPartStride) {
                 if (lane < kNeq)
 #pragma unroll
-                    for (int w = 0; w < kRedThreads / 64; ++w) sum += red[w][lane];
+                    for (int w = 0; w < kThreads / 64; ++w) sum += red[w][lane];
                 st_u64_sc1(part + (size_t)c * kPartStride + lane,
                            (unsigned long long)__double_as_longlong(sum));
             }
@@ -1494,41 +1565,12 @@ __global__ __launch_bounds__(kRedThreads, 2) void k_icp_coop(const int16_t* __re
             timeout = true;
             break;
         }
-        // ---- every workgroup sums the pair's partials in k_icp's fixed order
-        {
-            const __amdgpu_buffer_rsrc_t rpart = __builtin_amdgcn_make_buffer_rsrc(
-                part, (short)0, G * kPartStride * (int)sizeof(double), 0x00020000);
-            const int t = threadIdx.x;
-            const int jc = t / kPieces, q = t - jc * kPieces;
-            if (jc < kSumCols) {
-                double s0 = 0.0, s1 = 0.0;
-                for (int bb = jc; bb < G; bb += 16 * kSumCols) {
-                    u4v v[16];
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const int b = bb + i * kSumCols;
-                        v[i] = b < G ? __builtin_bit_cast(
-                                           u4v, __builtin_amdgcn_raw_buffer_load_b128(
-                                                    rpart, (b * kPartStride + 2 * q) * 8, 0, 16))
-                                     : u4v{0u, 0u, 0u, 0u};
-                    }
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        s0 += __hiloint2double((int)v[i].y, (int)v[i].x);
-                        s1 += __hiloint2double((int)v[i].w, (int)v[i].z);
-                    }
-                }
-                colsum[jc][2 * q] = s0;
-                colsum[jc][2 * q + 1] = s1;
-            }
-        }
-        __syncthreads();
+        // ---- every workgroup sums the pair's partials in the same fixed order
+        const __amdgpu_buffer_rsrc_t rpart = __builtin_amdgcn_make_buffer_rsrc(
+            part, (short)0, G * kPartStride * (int)sizeof(double), 0x00020000);
+        const double tsum = sum_pair_rows(rpart, G, colsum);
         COOP_MARK(k, 6);
         if (wave == 0) {
-            double tsum = 0.0;
-            if (lane < kNeq)
-#pragma unroll
-                for (int jj = 0; jj < kSumCols; ++jj) tsum += colsum[jj][lane];
             double neq[kNeq];
 #pragma unroll
             for (int qq = 0; qq < kNeq; ++qq) neq[qq] = readlane64(tsum, qq);
@@ -1541,8 +1583,11 @@ __global__ __launch_bounds__(kRedThreads, 2) void k_icp_coop(const int16_t* __re
                     cs.stats[((size_t)p * cs.iters + k) * 2 + 1] = neq[27];
                 }
                 double xi[6];
+                COOP_MARK(k, 8);
                 const int st = solve6(neq, xi);
+                COOP_MARK(k, 9);
                 if (st == 0) se3_exp_left(xi, Tm);
+                COOP_MARK(k, 10);
                 st_acc |= st;
 #pragma unroll
                 for (int qq = 0; qq < 12; ++qq) {
@@ -1643,12 +1688,13 @@ struct youth_icp_ctx {
     int n_cu = 0;
     // small batches: k_icp_coop (youth_icp_create reads the knobs)
     bool coop = true;                // YOUTH_ICP_NO_COOP=1 disables
-    int coop_steps = 2;              // YOUTH_ICP_COOP_STEPS: min 1024-px steps per workgroup
+    int coop_px = 0;                 // YOUTH_ICP_COOP_PX: force pixels per lane (0: plan)
+    int coop_threads = 512;          // YOUTH_ICP_COOP_THREADS=256: one wave per SIMD
     int coop_max_pairs = 4;          // YOUTH_ICP_COOP_MAX_PAIRS (<= kCoopMaxPairs)
-    int coop_bpc[4][kCoopMaxSteps] = {};  // occupancy of k_icp_coop<fast, aligned, steps>
+    int coop_bpc[2][kCoopMaxPx + 1] = {};  // occupancy of k_icp_coop<fast> at npx (LDS)
     unsigned* d_coop = nullptr;      // 2 counter sets of kCoopSetWords
     int coop_par = 0;                // set used by the next coop call
-    int last_coop_G = 0, last_coop_steps = 0;
+    int last_coop_G = 0, last_coop_px = 0;
 
     int last_pairs = 0;
     int last_iters = 0;
@@ -1838,48 +1884,47 @@ static int launch_reduce(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, P
     return ev_end(c, s, &ep);
 }
 
-// Small-batch plan: the fewest 1024-px steps per workgroup (>= coop_steps)
-// whose n_pairs x G workgroups fit the co-resident capacity with one block
-// per CU to spare (cooperative launch admission, MI355X_MICROARCH.md).
-static bool coop_plan(const youth_icp_ctx* c, int n_pairs, int var, int* steps_out, int* G_out)
+// Small-batch plan.  One wave per SIMD issues a wave64 instruction in >= 4
+// cycles, so a pair's pixel phase costs ~ npx x (workgroups per CU): pick
+// the npx (source pixels per lane) minimising npx x ceil(n_pairs G / CUs)
+// among those whose n_pairs x G workgroups fit the co-resident capacity with
+// one block per CU to spare (cooperative launch admission,
+// MI355X_MICROARCH.md); ties go to the larger npx (fewer partials to sum).
+static size_t coop_lds(int npx, int threads) { return (size_t)3 * npx * threads * sizeof(float); }
+
+static bool coop_plan(const youth_icp_ctx* c, int n_pairs, int* npx_out, int* G_out)
 {
     if (!c->coop || n_pairs > c->coop_max_pairs || n_pairs > kCoopMaxPairs) return false;
-    for (int st = c->coop_steps; st <= kCoopMaxSteps; ++st) {
-        const int chunk = st * kRedStep;
+    const int v = c->fast ? 1 : 0;
+    long long best = -1;
+    for (int npx = 1; npx <= kCoopMaxPx; ++npx) {
+        if (c->coop_px && npx != c->coop_px) continue;
+        const int chunk = npx * c->coop_threads;
         const int G = (c->N + chunk - 1) / chunk;
-        const long long cap = (long long)c->n_cu * (c->coop_bpc[var][st - 1] - 1);
-        if ((long long)G * n_pairs <= cap) {
-            *steps_out = st;
+        const long long wgs = (long long)G * n_pairs;
+        // VGPR-limited occupancy: k_icp_coop's SGPR count (106) admits 6
+        // 256-thread blocks per CU (MI355X_MICROARCH.md residency formula),
+        // more than the API's VGPR answer, so the API count is exact here
+        const int bpc = c->coop_bpc[v][npx];
+        if (bpc < 1 || wgs > (long long)c->n_cu * bpc) continue;
+        const long long cost = (long long)npx * ((wgs + c->n_cu - 1) / c->n_cu);
+        if (best < 0 || cost <= best) {
+            best = cost;
+            *npx_out = npx;
             *G_out = G;
-            return true;
         }
     }
-    return false;
+    return best >= 0;
 }
 
-template <bool kFast, bool kAligned>
-static const void* coop_kernel(int steps)
+static const void* coop_kernel(bool fast, int threads)
 {
-    switch (steps) {
-    case 1: return (const void*)k_icp_coop<kFast, kAligned, 1>;
-    case 2: return (const void*)k_icp_coop<kFast, kAligned, 2>;
-    case 3: return (const void*)k_icp_coop<kFast, kAligned, 3>;
-    default: return (const void*)k_icp_coop<kFast, kAligned, 4>;
-    }
-}
-
-static const void* coop_kernel(int var, int steps)
-{
-    switch (var) {
-    case 0: return coop_kernel<false, false>(steps);
-    case 1: return coop_kernel<false, true>(steps);
-    case 2: return coop_kernel<true, false>(steps);
-    default: return coop_kernel<true, true>(steps);
-    }
+    if (threads == 256) return fast ? (const void*)k_icp_coop<true, 256> : (const void*)k_icp_coop<false, 256>;
+    return fast ? (const void*)k_icp_coop<true, 512> : (const void*)k_icp_coop<false, 512>;
 }
 
 static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, PairMap pm,
-                       int n_pairs, const double* dTi, float* d_T_out, int var, int steps, int G)
+                       int n_pairs, const double* dTi, float* d_T_out, int npx, int G)
 {
     const int iters = c->prm.iters;
     int rc = ensure_partials(c, (size_t)2 * n_pairs * G * kPartStride);
@@ -1888,7 +1933,7 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
     unsigned* set_next = c->d_coop + (size_t)(c->coop_par ^ 1) * kCoopSetWords;
     c->coop_par ^= 1;
     CoopState cs{dTi, c->d_T64, c->d_T32, c->d_status, c->d_stats, d_T_out,
-                 set, set_next, c->d_head, iters, n_pairs, G, steps * kRedStep};
+                 set, set_next, c->d_head, iters, n_pairs, G, npx};
     const float4* recs = c->d_rec;
     size_t P = c->P;
     int W = c->W, H = c->H;
@@ -1901,10 +1946,11 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
     EventPair ep{};
     rc = ev_begin(c, s, &ep, 0);
     if (rc) return rc;
-    HIP_TRY(hipLaunchCooperativeKernel(coop_kernel(var, steps), dim3((unsigned)(n_pairs * G)),
-                                       dim3(kRedThreads), args, 0, s));
+    HIP_TRY(hipLaunchCooperativeKernel(coop_kernel(c->fast, c->coop_threads),
+                                       dim3((unsigned)(n_pairs * G)), dim3(c->coop_threads), args,
+                                       (unsigned)coop_lds(npx, c->coop_threads), s));
     c->last_coop_G = G;
-    c->last_coop_steps = steps;
+    c->last_coop_px = npx;
     return ev_end(c, s, &ep);
 }
 
@@ -1926,11 +1972,9 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
         dTi = c->d_Tinit;
     }
     {
-        const bool aligned = (reinterpret_cast<uintptr_t>(dsrc) % 8 == 0) && (c->W % 4 == 0);
-        const int var = (c->fast ? 2 : 0) | (aligned ? 1 : 0);
-        int steps = 0, G = 0;
-        if (iters > 0 && coop_plan(c, n_pairs, var, &steps, &G)) {
-            rc = launch_coop(c, s, dsrc, pm, n_pairs, dTi, d_T_out, var, steps, G);
+        int npx = 0, G = 0;
+        if (iters > 0 && coop_plan(c, n_pairs, &npx, &G)) {
+            rc = launch_coop(c, s, dsrc, pm, n_pairs, dTi, d_T_out, npx, G);
             if (rc) return rc;
             if (exported) *exported = d_T_out != nullptr;
             c->last_pairs = n_pairs;
@@ -2150,19 +2194,21 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         }
         const char* np = getenv("YOUTH_ICP_NO_PERSISTENT");
         c->persistent = !(np && *np && *np != '0');
-        for (int v = 0; v < 4; ++v)
-            for (int st = 1; st <= kCoopMaxSteps; ++st) {
+        const char* cth = getenv("YOUTH_ICP_COOP_THREADS");
+        if (cth && atoi(cth) == 256) c->coop_threads = 256;
+        for (int v = 0; v < 2; ++v)
+            for (int npx = 1; npx <= kCoopMaxPx; ++npx) {
                 int nb = 0;
-                if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, coop_kernel(v, st),
-                                                                      kRedThreads, 0)) !=
-                    hipSuccess)
+                if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                         &nb, coop_kernel(v != 0, c->coop_threads), c->coop_threads,
+                         coop_lds(npx, c->coop_threads))) != hipSuccess)
                     return fail("occupancy coop", e);
-                c->coop_bpc[v][st - 1] = nb;
+                c->coop_bpc[v][npx] = nb;
             }
         const char* nc = getenv("YOUTH_ICP_NO_COOP");
         c->coop = !(nc && *nc && *nc != '0');
-        const char* cst = getenv("YOUTH_ICP_COOP_STEPS");
-        if (cst && atoi(cst) >= 1 && atoi(cst) <= kCoopMaxSteps) c->coop_steps = atoi(cst);
+        const char* cpx = getenv("YOUTH_ICP_COOP_PX");
+        if (cpx && atoi(cpx) >= 1 && atoi(cpx) <= kCoopMaxPx) c->coop_px = atoi(cpx);
         const char* cmp = getenv("YOUTH_ICP_COOP_MAX_PAIRS");
         if (cmp && atoi(cmp) >= 0) c->coop_max_pairs = atoi(cmp);
     }

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Small-batch A/B on the GPU box: k_icp_coop (steps 2..4) vs the persistent
+# Small-batch A/B on the GPU box: k_icp_coop (planned, and PXS="5 8 .." forced
+# pixels per lane) vs the persistent
 # k_icp (YOUTH_ICP_NO_COOP=1), pairs 1/2/4, interleaved in one process tree.
 # Usage: tools/coop_sweep.sh [rounds]
 set -uo pipefail
@@ -15,8 +16,10 @@ for r in $(seq 1 $R); do
   for np in 1 2 4; do
     S=$((200 / np + 20))
     one "pairs=$np persistent" YOUTH_ICP_NO_COOP=1 -- --pairs-per-gpu $np --steps $S --warmup 20 || exit 1
-    for st in 2 3 4; do
-      one "pairs=$np coop steps=$st" YOUTH_ICP_COOP_STEPS=$st YOUTH_ICP_COOP_MAX_PAIRS=16 -- --pairs-per-gpu $np --steps $S --warmup 20 || exit 1
+    one "pairs=$np coop planned 512" YOUTH_ICP_COOP_MAX_PAIRS=16 -- --pairs-per-gpu $np --steps $S --warmup 20 || exit 1
+    one "pairs=$np coop planned 256" YOUTH_ICP_COOP_THREADS=256 YOUTH_ICP_COOP_MAX_PAIRS=16 -- --pairs-per-gpu $np --steps $S --warmup 20 || exit 1
+    for px in ${PXS:-}; do
+      one "pairs=$np coop px=$px" YOUTH_ICP_COOP_PX=$px YOUTH_ICP_COOP_MAX_PAIRS=16 -- --pairs-per-gpu $np --steps $S --warmup 20 || exit 1
     done
   done
 done

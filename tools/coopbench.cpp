@@ -1,6 +1,6 @@
 // coopbench — where an iteration of k_icp_coop spends its time (one pair).
 //
-// Build: make -C tools coopbench      Run (GPU box): tools/coopbench [pairs] [steps]
+// Build: make -C tools coopbench      Run (GPU box): tools/coopbench [pairs] [px_per_lane]
 // Includes the production translation unit with YOUTH_COOP_PHASES, so thread
 // 0 of every workgroup stamps s_memrealtime (100 MHz) at 8 points of every
 // iteration: 0 start, 1 pixel loop done, 2 workgroup reduction done,
@@ -34,7 +34,7 @@ static double median(std::vector<double> v)
 int main(int argc, char** argv)
 {
     const int n = argc > 1 ? atoi(argv[1]) : 1;
-    if (argc > 2) setenv("YOUTH_ICP_COOP_STEPS", argv[2], 1);
+    if (argc > 2) setenv("YOUTH_ICP_COOP_PX", argv[2], 1);
     setenv("YOUTH_ICP_COOP_MAX_PAIRS", "16", 1);
     const int W = 640, H = 480, N = W * H;
     youth_intrinsics K = youth_default_intrinsics(W, H);
@@ -58,25 +58,25 @@ int main(int argc, char** argv)
     for (int r = 0; r < 50; ++r)
         if (youth_icp_align_pairs_device(c, d_s, d_d, n, nullptr, d_T, nullptr)) return 1;
     CK(hipDeviceSynchronize());
-    const int G = c->last_coop_G, steps = c->last_coop_steps;
+    const int G = c->last_coop_G, npx = c->last_coop_px;
     if (!G) {
         fprintf(stderr, "coop path not taken for %d pairs\n", n);
         return 1;
     }
     const int blocks = G * n, iters = prm.iters;
     unsigned long long* d_ph;
-    const size_t words = (size_t)blocks * 32 * 8;
+    const size_t words = (size_t)blocks * 32 * 16;
     CK(hipMalloc(&d_ph, words * 8));
     CK(hipMemset(d_ph, 0, words * 8));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(coop_phase), &d_ph, sizeof(d_ph)));
     const int reps = 20;
-    std::vector<double> ph[8], hop, spread, total;
+    std::vector<double> ph[8], hop, spread, total, sol[3], wv[4];
     std::vector<unsigned long long> h(words);
     for (int r = 0; r < reps; ++r) {
         if (youth_icp_align_pairs_device(c, d_s, d_d, n, nullptr, d_T, nullptr)) return 1;
         CK(hipDeviceSynchronize());
         CK(hipMemcpy(h.data(), d_ph, words * 8, hipMemcpyDeviceToHost));
-        auto at = [&](int b, int k, int s) { return (double)h[((size_t)b * 32 + k) * 8 + s]; };
+        auto at = [&](int b, int k, int s) { return (double)h[((size_t)b * 32 + k) * 16 + s]; };
         for (int k = 1; k < iters; ++k) {
             for (int p = 0; p < n; ++p) {
                 double last3 = 0, first4 = 1e300, mn0 = 1e300, mx0 = 0;
@@ -90,6 +90,16 @@ int main(int argc, char** argv)
                     mx0 = std::max(mx0, at(b, k, 0));
                 }
                 hop.push_back((first4 - last3) * 10.0);
+                const int b0 = p * G;
+                sol[0].push_back((at(b0, k, 8) - at(b0, k, 6)) * 10.0);
+                sol[1].push_back((at(b0, k, 9) - at(b0, k, 8)) * 10.0);
+                sol[2].push_back((at(b0, k, 10) - at(b0, k, 9)) * 10.0);
+                for (int cc = 0; cc < G; ++cc) {
+                    const int b = p * G + cc;
+                    wv[0].push_back((at(b, k, 11) - at(b, k, 1)) * 10.0);  // wave 0 reduce-scatter
+                    for (int w = 1; w < 4; ++w)                             // wave w loop end - wave 0's
+                        wv[w].push_back((at(b, k, 11 + w) - at(b, k, 1)) * 10.0);
+                }
                 spread.push_back((mx0 - mn0) * 10.0);
             }
         }
@@ -98,8 +108,8 @@ int main(int argc, char** argv)
     }
     const char* names[8] = {"pixel loop", "wg reduction", "publish+arrive", "poll (all arrived)",
                             "barrier", "sum partials", "solve+barrier", "loop back"};
-    printf("pairs %d  G %d  steps %d  (ns, medians over workgroups x iterations 1..%d x %d reps)\n",
-           n, G, steps, iters - 1, reps);
+    printf("pairs %d  G %d  px/lane %d  (ns, medians over workgroups x iterations 1..%d x %d reps)\n",
+           n, G, npx, iters - 1, reps);
     double acc = 0;
     for (int s = 0; s < 8; ++s) {
         const double m = median(ph[s]);
@@ -110,6 +120,10 @@ int main(int argc, char** argv)
     printf("  %-22s %8.0f\n", "iteration (chunk 0)", median(total));
     printf("  %-22s %8.0f\n", "hand-off hop", median(hop));
     printf("  %-22s %8.0f\n", "start spread", median(spread));
+    printf("  wave 0 reduce-scatter %6.0f   pixel loop end of waves 1..3 - wave 0's: %6.0f %6.0f %6.0f\n",
+           median(wv[0]), median(wv[1]), median(wv[2]), median(wv[3]));
+    printf("  chunk-0 lane 0: column sums -> solve %6.0f   LDL^T solve %6.0f   SE(3) exp %6.0f\n",
+           median(sol[0]), median(sol[1]), median(sol[2]));
     youth_icp_destroy(c);
     return 0;
 }
