@@ -199,7 +199,7 @@ int oracle_solve(const double neq[ORACLE_NEQ], double xi[6])
     for (int i = 0; i < 6; ++i) y[i] = y[i] * Dinv[i];
     for (int i = 5; i >= 0; --i) {
         double s = y[i];
-        for (int m = i + 1; m < 6; ++m) s -= L[m][i] * x[m];
+        for (int m = 5; m > i; --m) s -= L[m][i] * x[m];  /* m decreasing */
         x[i] = s;
     }
     for (int i = 0; i < 6; ++i) xi[i] = x[i];

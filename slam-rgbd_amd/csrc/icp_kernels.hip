@@ -80,6 +80,21 @@ struct FastK {
     float rfx, rfy, rds;
 };
 
+// 64-bit lane helpers (two 32-bit halves)
+__device__ __forceinline__ double join64(unsigned lo, unsigned hi)
+{
+    return __hiloint2double((int)hi, (int)lo);
+}
+__device__ __forceinline__ unsigned lo32(double x) { return (unsigned)__double2loint(x); }
+__device__ __forceinline__ unsigned hi32(double x) { return (unsigned)__double2hiint(x); }
+
+// lane `l`'s value in every lane (wave-uniform l: two v_readlane into SGPRs)
+__device__ __forceinline__ double readlane64(double x, int l)
+{
+    return join64((unsigned)__builtin_amdgcn_readlane((int)lo32(x), l),
+                  (unsigned)__builtin_amdgcn_readlane((int)hi32(x), l));
+}
+
 // q = RN(n * rd); r = n - q d (exact, fma); q + r rd (one rounding).
 // Equal to RN(n / d) wherever k_verify_fastdiv found no mismatch.
 __device__ __forceinline__ float div_fast(float n, float d, float rd)
@@ -476,7 +491,7 @@ __device__ int solve6(const double* neq, double xi[6])
     for (int i = 0; i < 6; ++i) y[i] = y[i] * Dinv[i];
     for (int i = 5; i >= 0; --i) {
         double s = y[i];
-        for (int m = i + 1; m < 6; ++m) s -= L[m][i] * x[m];
+        for (int m = 5; m > i; --m) s -= L[m][i] * x[m];
         x[i] = s;
     }
     for (int i = 0; i < 6; ++i) xi[i] = x[i];
@@ -530,6 +545,130 @@ __device__ void se3_exp_left(const double xi[6], double* T)
             O[i * 4 + j] = s;
         }
     for (int i = 0; i < 12; ++i) T[i] = O[i];
+}
+
+// Spec a10 by ONE wave (all 64 lanes call it): solve6 + se3_exp_left with
+// their per-element operations and order (bit-identical results), spread
+// over lanes because a lone lane pays the wave's full issue cost for every
+// fp64 instruction (~2.2 us per iteration on one lane, tools/coopbench):
+//   * lane i < 6 owns row i of A and L: column j of the factorisation is one
+//     step (the pivot d_j and every L[i][j] together), L[j][m] and d_j are
+//     broadcast with v_readlane;
+//   * forward / back substitution: lane i owns y_i / x_i and subtracts
+//     L[i][m] y_m (m increasing) / L[m][i] x_m (m decreasing) as each
+//     becomes final;
+//   * lane l < 12 computes output entry (l / 4, l % 4) of exp(xi^) T.
+// neq (LDS, kNeq): the pair's sums; T64 (LDS, 12): pose in/out; T32 (LDS,
+// 12): fp32 copy out; Lsh (LDS, 36): scratch.  Returns the status bits; the
+// pose is updated only when they are 0.
+__device__ __forceinline__ int tri6(int a, int b)  // upper-triangle index, a <= b
+{
+    return a * 6 - (a * (a - 1)) / 2 + (b - a);
+}
+
+__device__ int solve_update_wave(const double* neq, double* T64, float* T32, double* Lsh, int lane)
+{
+    if (!(neq[28] >= 6.0)) return YOUTH_STATUS_FEW_MATCHES;
+    const int i = lane < 6 ? lane : 5;
+    double maxd = 0.0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+        const double da = neq[tri6(a, a)];
+        if (da > maxd) maxd = da;
+    }
+    if (!(maxd > 0.0)) return YOUTH_STATUS_DEGENERATE;
+    const double eps = 1e-12 * maxd;
+    double Ar[6], Lr[6], D[6], Dinv[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        Ar[j] = neq[i <= j ? tri6(i, j) : tri6(j, i)];
+        Lr[j] = 0.0;
+    }
+    // LDL^T, column j: lane i computes A[i][j] - sum_m (L[i][m] L[j][m]) D[m]
+    // (lane j: the pivot d_j); L[i][j] = s / d_j below the diagonal
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        double sj = Ar[j];
+#pragma unroll
+        for (int m = 0; m < j; ++m) sj -= (Lr[m] * readlane64(Lr[m], j)) * D[m];
+        const double d = readlane64(sj, j);
+        if (!(d > eps)) return YOUTH_STATUS_DEGENERATE;
+        D[j] = d;
+        Dinv[j] = 1.0 / d;  // one divide per pivot; every use multiplies
+        Lr[j] = lane > j ? sj * Dinv[j] : (lane == j ? 1.0 : 0.0);
+    }
+    // forward: y_i = (-b_i - sum_{m<i} L[i][m] y_m) / d_i
+    double y = -neq[21 + i];
+#pragma unroll
+    for (int m = 0; m < 6; ++m) {
+        const double ym = readlane64(y, m);
+        y = lane > m ? y - Lr[m] * ym : y;
+    }
+    double dinv = Dinv[0];
+#pragma unroll
+    for (int j = 1; j < 6; ++j) dinv = i == j ? Dinv[j] : dinv;
+    y = y * dinv;
+    // back: x_i = y_i - sum_{m>i} L[m][i] x_m, m decreasing (column i of L via LDS)
+    if (lane < 6) {
+#pragma unroll
+        for (int j = 0; j < 6; ++j) Lsh[lane * 6 + j] = Lr[j];
+    }
+    double x = y;
+#pragma unroll
+    for (int m = 5; m >= 0; --m) {
+        const double xm = readlane64(x, m);
+        const double Lmi = Lsh[m * 6 + i];
+        x = lane < m ? x - Lmi * xm : x;
+    }
+    double xi[6];
+#pragma unroll
+    for (int m = 0; m < 6; ++m) xi[m] = readlane64(x, m);
+
+    // T <- exp(xi^) T (se3_exp_left), one output entry per lane
+    const double wx = xi[0], wy = xi[1], wz = xi[2];
+    const double th2 = (wx * wx + wy * wy) + wz * wz;
+    double a, b, c;
+    if (th2 < 0x1p-7) {  // spec a10: Taylor in th2 (oracle_se3_exp: same fma chain)
+        const double x2 = th2;
+        a = fma(x2, fma(x2, fma(x2, fma(x2, fma(x2, -0x1.ae64567f544e4p-26, 0x1.71de3a556c734p-19),
+                                          -0x1.a01a01a01a01ap-13), 0x1.1111111111111p-7),
+                        -0x1.5555555555555p-3), 0x1.0000000000000p+0);
+        b = fma(x2, fma(x2, fma(x2, fma(x2, fma(x2, -0x1.1eed8eff8d898p-29, 0x1.27e4fb7789f5cp-22),
+                                          -0x1.a01a01a01a01ap-16), 0x1.6c16c16c16c17p-10),
+                        -0x1.5555555555555p-5), 0x1.0000000000000p-1);
+        c = fma(x2, fma(x2, fma(x2, fma(x2, fma(x2, -0x1.6124613a86d09p-33, 0x1.ae64567f544e4p-26),
+                                          -0x1.71de3a556c734p-19), 0x1.a01a01a01a01ap-13),
+                        -0x1.1111111111111p-7), 0x1.5555555555555p-3);
+    } else {
+        const double th = sqrt(th2);
+        double sn, co;
+        sincos(th, &sn, &co);
+        a = sn / th;
+        b = (1.0 - co) / th2;
+        c = (th - sn) / (th2 * th);
+    }
+    const double Km[3][3] = {{0.0, -wz, wy}, {wz, 0.0, -wx}, {-wy, wx, 0.0}};
+    const int l = lane < 12 ? lane : 11;
+    const int r = l >> 2, col = l & 3;
+    double Kr[3];  // row r of Km
+#pragma unroll
+    for (int k = 0; k < 3; ++k) Kr[k] = r == 0 ? Km[0][k] : (r == 1 ? Km[1][k] : Km[2][k]);
+    double Er[3], Vr[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double K2 = (Kr[0] * Km[0][k] + Kr[1] * Km[1][k]) + Kr[2] * Km[2][k];
+        const double I = (r == k) ? 1.0 : 0.0;
+        Er[k] = (I + a * Kr[k]) + b * K2;
+        Vr[k] = (I + b * Kr[k]) + c * K2;
+    }
+    const double Er3 = (Vr[0] * xi[3] + Vr[1] * xi[4]) + Vr[2] * xi[5];
+    double o = (Er[0] * T64[0 * 4 + col] + Er[1] * T64[1 * 4 + col]) + Er[2] * T64[2 * 4 + col];
+    if (col == 3) o += Er3;
+    if (lane < 12) {
+        T64[lane] = o;
+        T32[lane] = (float)o;
+    }
+    return 0;
 }
 
 // Sum the nblk partials of pair p in a fixed order: lanes 0..28 take the
@@ -809,20 +948,6 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
 //   m = 8, 2, 1: DPP (row_ror:8, quad_perm) moves; m = 4: ds_swizzle xor.
 // No LDS bpermute; the partners (lane ^ m) and the add order are unchanged,
 // so the sums are bit-identical to the shuffle form.
-__device__ __forceinline__ double join64(unsigned lo, unsigned hi)
-{
-    return __hiloint2double((int)hi, (int)lo);
-}
-__device__ __forceinline__ unsigned lo32(double x) { return (unsigned)__double2loint(x); }
-__device__ __forceinline__ unsigned hi32(double x) { return (unsigned)__double2hiint(x); }
-
-// lane `l`'s value in every lane (wave-uniform l: two v_readlane into SGPRs)
-__device__ __forceinline__ double readlane64(double x, int l)
-{
-    return join64((unsigned)__builtin_amdgcn_readlane((int)lo32(x), l),
-                  (unsigned)__builtin_amdgcn_readlane((int)hi32(x), l));
-}
-
 template <int kM>
 __device__ __forceinline__ double xchg_small(double x)
 {
@@ -1150,7 +1275,10 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
 {
     __shared__ double red[kRedThreads / 64][kNeq];
     __shared__ double colsum[kSumCols][kPartStride];
+    __shared__ double sh_neq[kNeq];
+    __shared__ double sh_L[36];
     __shared__ double sh_T64[12];
+    __shared__ float sh_T32n[12];
     __shared__ int sh_item;
     __shared__ int sh_last;
     __shared__ float sh_T[12];
@@ -1228,33 +1356,23 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
                     (long long)ld_u64_sc1(is.T64 + (size_t)p * 16 + (threadIdx.x - 64)));
             const double tsum = sum_pair_rows(rpart, is.nblk, colsum);
             if (wave == 0) {
-                double neq[kNeq];
-#pragma unroll
-                for (int qq = 0; qq < kNeq; ++qq) neq[qq] = readlane64(tsum, qq);
-                if (lane == 0) {
-                    double Tm[16];
-#pragma unroll
-                    for (int qq = 0; qq < 12; ++qq) Tm[qq] = sh_T64[qq];
-                    if (is.stats) {
-                        is.stats[((size_t)p * is.iters + k) * 2 + 0] = neq[28];
-                        is.stats[((size_t)p * is.iters + k) * 2 + 1] = neq[27];
-                    }
-                    double xi[6];
-                    const int st = solve6(neq, xi);
-                    if (st == 0) se3_exp_left(xi, Tm);
-                    if (st) __hip_atomic_fetch_or(is.status + p, st, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-                    for (int qq = 0; qq < 12; ++qq)
-                        st_u64_sc1(is.T64 + (size_t)p * 16 + qq,
-                                   (unsigned long long)__double_as_longlong(Tm[qq]));
-                    for (int qq = 0; qq < 12; qq += 2)
-                        st_u64_sc1(is.T32 + (size_t)p * 12 + qq,
-                                   (unsigned long long)__float_as_uint((float)Tm[qq]) |
-                                       ((unsigned long long)__float_as_uint((float)Tm[qq + 1])
-                                        << 32));
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    st_u32_sc1(is.epoch + p, (unsigned)(k + 1));
+                if (lane < kNeq) sh_neq[lane] = tsum;
+                if (is.stats && lane == 0) {
+                    is.stats[((size_t)p * is.iters + k) * 2 + 0] = readlane64(tsum, 28);
+                    is.stats[((size_t)p * is.iters + k) * 2 + 1] = readlane64(tsum, 27);
                 }
+                const int st = solve_update_wave(sh_neq, sh_T64, sh_T32n, sh_L, lane);
+                if (st && lane == 0)
+                    __hip_atomic_fetch_or(is.status + p, st, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+                // publish: lanes < 12 store the pose (sc1), the wave drains, then the epoch
+                if (lane < 12) {
+                    st_u64_sc1(is.T64 + (size_t)p * 16 + lane,
+                               (unsigned long long)__double_as_longlong(sh_T64[lane]));
+                    st_u32_sc1(is.T32 + (size_t)p * 12 + lane, __float_as_uint(sh_T32n[lane]));
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (lane == 0) st_u32_sc1(is.epoch + p, (unsigned)(k + 1));
             }
         }
         // ---- next item (this workgroup has published: waiting is safe)
@@ -1435,6 +1553,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
     extern __shared__ float coop_src[];  // [3][npx][kThreads]
     __shared__ double red[kThreads / 64][kNeq];
     __shared__ double colsum[kSumCols][kPartStride];
+    __shared__ double sh_neq[kNeq];
+    __shared__ double sh_L[36];
     __shared__ double sh_T64[12];
     __shared__ float sh_T[12];
     __shared__ int sh_stop;
@@ -1571,30 +1691,15 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
         const double tsum = sum_pair_rows(rpart, G, colsum);
         COOP_MARK(k, 6);
         if (wave == 0) {
-            double neq[kNeq];
-#pragma unroll
-            for (int qq = 0; qq < kNeq; ++qq) neq[qq] = readlane64(tsum, qq);
-            if (lane == 0) {
-                double Tm[16];
-#pragma unroll
-                for (int qq = 0; qq < 12; ++qq) Tm[qq] = sh_T64[qq];
-                if (c == 0 && cs.stats) {
-                    cs.stats[((size_t)p * cs.iters + k) * 2 + 0] = neq[28];
-                    cs.stats[((size_t)p * cs.iters + k) * 2 + 1] = neq[27];
-                }
-                double xi[6];
-                COOP_MARK(k, 8);
-                const int st = solve6(neq, xi);
-                COOP_MARK(k, 9);
-                if (st == 0) se3_exp_left(xi, Tm);
-                COOP_MARK(k, 10);
-                st_acc |= st;
-#pragma unroll
-                for (int qq = 0; qq < 12; ++qq) {
-                    sh_T64[qq] = Tm[qq];
-                    sh_T[qq] = (float)Tm[qq];
-                }
+            if (lane < kNeq) sh_neq[lane] = tsum;
+            if (c == 0 && cs.stats && lane == 0) {
+                cs.stats[((size_t)p * cs.iters + k) * 2 + 0] = readlane64(tsum, 28);
+                cs.stats[((size_t)p * cs.iters + k) * 2 + 1] = readlane64(tsum, 27);
             }
+            COOP_MARK(k, 8);
+            st_acc |= solve_update_wave(sh_neq, sh_T64, sh_T, sh_L, lane);
+            COOP_MARK(k, 9);
+            COOP_MARK(k, 10);
         }
         __syncthreads();
         COOP_MARK(k, 7);
