@@ -327,31 +327,29 @@ __global__ void k_selftest_normalize(unsigned long long n, unsigned long long se
 // n = normalize((P(u+1)-P(u-1)) x (P(v+1)-P(v-1))); (0,0,0) on the 1-px
 // border, if the centre or any of the 4 neighbours is invalid, or if the
 // cross product is zero; oriented so n.P <= 0.
-template <bool kFast, bool kWide>
-__global__ __launch_bounds__(kPrepThreads) void k_prep(const int16_t* __restrict__ depth, int out0,
-                                                      int W, int H, size_t P, Intr K, FastK F,
-                                                      float4* __restrict__ recs,
-                                                      float* __restrict__ xyz)
+// One kTileW x kTH tile of target records (and optional X/Y/Z planes) by a
+// workgroup of kThreads: the (kTH+2) x (kTileW+2) back-projected
+// neighbourhood is staged in the LDS planes sX/sY/sZ ([kTH+2][kLdsW]), then
+// each thread forms the records of column tx = t & 63, rows ty, ty +
+// kThreads/64, ...  kSc1: records are stored write-through (16-byte sc1
+// buffer stores) for an in-launch hand-off (k_icp_coop).  Contains a
+// workgroup barrier (every thread must call it); a caller reusing the LDS
+// planes for another tile adds one more before it.
+template <bool kFast, bool kWide, bool kSc1, int kThreads, int kTH>
+__device__ __forceinline__ void prep_tile(const int16_t* __restrict__ dep, float4* __restrict__ R,
+                                          int W, int H, size_t P, const Intr& K, const FastK& F,
+                                          float* __restrict__ X, int x0, int y0, float* sX,
+                                          float* sY, float* sZ)
 {
-    __shared__ float sX[kLdsH][kLdsW];
-    __shared__ float sY[kLdsH][kLdsW];
-    __shared__ float sZ[kLdsH][kLdsW];
-
-    const int f = blockIdx.z;
-    const size_t N = (size_t)W * (size_t)H;
-    const int16_t* dep = depth + (size_t)f * N;
-    float4* R = recs + (size_t)(out0 + f) * P;
-    const int x0 = blockIdx.x * kTileW;
-    const int y0 = blockIdx.y * kTileH;
+    constexpr int kLH = kTH + 2;
     const int tx = threadIdx.x & 63;
     const int ty = threadIdx.x >> 6;
-
     if (kWide) {
         // W % 4 == 0 (and an 8-byte-aligned frame): columns [x0-4, x0+68) as
         // 18 aligned 8-byte words per halo row; each word's 4 pixels are all
         // inside or all outside the image, so no lane straddles an edge.
         constexpr int kWords = (kTileW + 8) / 4;  // 18
-        for (int e = threadIdx.x; e < kLdsH * kWords; e += kPrepThreads) {
+        for (int e = threadIdx.x; e < kLH * kWords; e += kThreads) {
             const int ly = e / kWords;
             const int m = e - ly * kWords;
             const int gy = y0 - 1 + ly;
@@ -366,36 +364,38 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const int16_t* __restrict
                 if (lx < 0 || lx >= kLdsW) continue;
                 float x, y, z;
                 backproject<kFast>(dv[q], c + q, gy, K, F, x, y, z);
-                sX[ly][lx] = x;
-                sY[ly][lx] = y;
-                sZ[ly][lx] = z;
+                sX[ly * kLdsW + lx] = x;
+                sY[ly * kLdsW + lx] = y;
+                sZ[ly * kLdsW + lx] = z;
             }
         }
     } else {
-        for (int e = threadIdx.x; e < kLdsH * kLdsW; e += kPrepThreads) {
+        for (int e = threadIdx.x; e < kLH * kLdsW; e += kThreads) {
             const int ly = e / kLdsW;
             const int lx = e - ly * kLdsW;
             const int gx = x0 - 1 + lx, gy = y0 - 1 + ly;
             float x = 0.0f, y = 0.0f, z = 0.0f;
             if (gx >= 0 && gx < W && gy >= 0 && gy < H)
                 backproject<kFast>(dep[(size_t)gy * W + gx], gx, gy, K, F, x, y, z);
-            sX[ly][lx] = x;
-            sY[ly][lx] = y;
-            sZ[ly][lx] = z;
+            sX[ly * kLdsW + lx] = x;
+            sY[ly * kLdsW + lx] = y;
+            sZ[ly * kLdsW + lx] = z;
         }
     }
     __syncthreads();
 
+    const __amdgpu_buffer_rsrc_t rrec =
+        __builtin_amdgcn_make_buffer_rsrc(R, (short)0, (int)(P * sizeof(float4)), 0x00020000);
 #pragma unroll
-    for (int k = 0; k < kTileH / 4; ++k) {
-        const int row = ty + 4 * k;
+    for (int k = 0; k < kTH / (kThreads / 64); ++k) {
+        const int row = ty + (kThreads / 64) * k;
         const int gx = x0 + tx, gy = y0 + row;
         if (gx >= W || gy >= H) continue;
         const size_t i = (size_t)gy * W + gx;
         const int ly = row + 1, lx = tx + 1;
-        const float px = sX[ly][lx], py = sY[ly][lx], pz = sZ[ly][lx];
-        if (xyz) {
-            float* X = xyz + (size_t)(out0 + f) * 3 * P;
+        const int o = ly * kLdsW + lx;
+        const float px = sX[o], py = sY[o], pz = sZ[o];
+        if (X) {
             X[i] = px;
             X[P + i] = py;
             X[2 * P + i] = pz;
@@ -404,14 +404,14 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const int16_t* __restrict
         bool has_n = false;
         const bool inner = gx > 0 && gy > 0 && gx < W - 1 && gy < H - 1;
         if (inner) {
-            const float zl = sZ[ly][lx - 1], zr = sZ[ly][lx + 1];
-            const float zu = sZ[ly - 1][lx], zd = sZ[ly + 1][lx];
+            const float zl = sZ[o - 1], zr = sZ[o + 1];
+            const float zu = sZ[o - kLdsW], zd = sZ[o + kLdsW];
             if (pz > 0.0f && zl > 0.0f && zr > 0.0f && zu > 0.0f && zd > 0.0f) {
-                const float ax = sX[ly][lx + 1] - sX[ly][lx - 1];
-                const float ay = sY[ly][lx + 1] - sY[ly][lx - 1];
+                const float ax = sX[o + 1] - sX[o - 1];
+                const float ay = sY[o + 1] - sY[o - 1];
                 const float az = zr - zl;
-                const float bx = sX[ly + 1][lx] - sX[ly - 1][lx];
-                const float by = sY[ly + 1][lx] - sY[ly - 1][lx];
+                const float bx = sX[o + kLdsW] - sX[o - kLdsW];
+                const float by = sY[o + kLdsW] - sY[o - kLdsW];
                 const float bz = zd - zu;
                 const float cx = ay * bz - az * by;
                 const float cy = az * bx - ax * bz;
@@ -442,8 +442,31 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const int16_t* __restrict
         // a target without a normal is stored as z = 0 ("invalid target"):
         // the spec's two tests "target valid" and "normal valid" become the
         // one tz > 0 test in the pixel loop (the Z plane keeps pz)
-        R[i] = make_float4(has_n ? pz : 0.0f, nx, ny, nz);
+        const float4 rec = make_float4(has_n ? pz : 0.0f, nx, ny, nz);
+        if (kSc1) {
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, rec), rrec,
+                                                   (int)(i * sizeof(float4)), 0, 16);
+        } else {
+            R[i] = rec;
+        }
     }
+}
+
+template <bool kFast, bool kWide>
+__global__ __launch_bounds__(kPrepThreads) void k_prep(const int16_t* __restrict__ depth, int out0,
+                                                      int W, int H, size_t P, Intr K, FastK F,
+                                                      float4* __restrict__ recs,
+                                                      float* __restrict__ xyz)
+{
+    __shared__ float sX[kLdsH * kLdsW];
+    __shared__ float sY[kLdsH * kLdsW];
+    __shared__ float sZ[kLdsH * kLdsW];
+    const int f = blockIdx.z;
+    const size_t N = (size_t)W * (size_t)H;
+    prep_tile<kFast, kWide, false, kPrepThreads, kTileH>(
+        depth + (size_t)f * N, recs + (size_t)(out0 + f) * P, W, H, P, K, F,
+        xyz ? xyz + (size_t)(out0 + f) * 3 * P : nullptr, blockIdx.x * kTileW, blockIdx.y * kTileH,
+        sX, sY, sZ);
 }
 
 // ----------------------------------------------------------------- k_solve --
@@ -566,7 +589,8 @@ __device__ __forceinline__ int tri6(int a, int b)  // upper-triangle index, a <=
     return a * 6 - (a * (a - 1)) / 2 + (b - a);
 }
 
-__device__ int solve_update_wave(const double* neq, double* T64, float* T32, double* Lsh, int lane)
+__device__ __forceinline__ int solve_update_wave(const double* neq, double* T64, float* T32,
+                                                double* Lsh, int lane)
 {
     if (!(neq[28] >= 6.0)) return YOUTH_STATUS_FEW_MATCHES;
     const int i = lane < 6 ? lane : 5;
@@ -669,6 +693,16 @@ __device__ int solve_update_wave(const double* neq, double* T64, float* T32, dou
         T32[lane] = (float)o;
     }
     return 0;
+}
+
+// Out-of-line copy for k_icp: inlined there, the solve's loop-invariant
+// constants are hoisted into the kernel prologue and spilled across the
+// pixel loop (128-VGPR budget), then reloaded from scratch on the pair's
+// critical path.  A call keeps its registers to itself.
+__device__ __attribute__((noinline)) int solve_update_wave_call(const double* neq, double* T64,
+                                                                float* T32, double* Lsh, int lane)
+{
+    return solve_update_wave(neq, T64, T32, Lsh, lane);
 }
 
 // Sum the nblk partials of pair p in a fixed order: lanes 0..28 take the
@@ -1108,8 +1142,8 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce(
 // Fixed-order sum of a pair's nblk partial rows (kPartStride doubles each,
 // written with sc1 stores by other workgroups, read with sc1 loads only).
 // Called by every thread of the workgroup.  Thread (column j, piece q) with
-// j < kSumCols loads rows j, j + 16, ... in batches of 16 16-byte pieces and
-// adds each batch as a pairwise tree (depth 4), batches in order; then wave 0
+// j < kSumCols loads rows j, j + 16, ... in batches of kBatch 16-byte pieces
+// and adds each batch as a pairwise tree, batches in order; then wave 0
 // lane l < kNeq adds the 16 column sums of value l as a pairwise tree.  The
 // tree keeps the dependent fp64 adds per value at ~8 + batches instead of the
 // 16 + rows of a running sum (the solve waits on it every iteration).  Returns
@@ -1124,6 +1158,7 @@ __device__ __forceinline__ double tree_sum(const double* v)
     }
 }
 
+template <int kBatch>
 __device__ __forceinline__ double sum_pair_rows(__amdgpu_buffer_rsrc_t rpart, int nblk,
                                                 double (*colsum)[kPartStride])
 {
@@ -1131,10 +1166,10 @@ __device__ __forceinline__ double sum_pair_rows(__amdgpu_buffer_rsrc_t rpart, in
     const int j = t / kPieces, q = t - j * kPieces;
     if (j < kSumCols) {
         double s0 = 0.0, s1 = 0.0;
-        for (int bb = j; bb < nblk; bb += 16 * kSumCols) {
-            u4v v[16];
+        for (int bb = j; bb < nblk; bb += kBatch * kSumCols) {
+            u4v v[kBatch];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
+            for (int i = 0; i < kBatch; ++i) {
                 const int b = bb + i * kSumCols;
                 // aux 16 = sc1 (bypass this CU's L1: written by other CUs)
                 v[i] = b < nblk ? __builtin_bit_cast(
@@ -1142,14 +1177,14 @@ __device__ __forceinline__ double sum_pair_rows(__amdgpu_buffer_rsrc_t rpart, in
                                                rpart, (b * kPartStride + 2 * q) * 8, 0, 16))
                                 : u4v{0u, 0u, 0u, 0u};
             }
-            double a0[16], a1[16];
+            double a0[kBatch], a1[kBatch];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
+            for (int i = 0; i < kBatch; ++i) {
                 a0[i] = __hiloint2double((int)v[i].y, (int)v[i].x);
                 a1[i] = __hiloint2double((int)v[i].w, (int)v[i].z);
             }
-            s0 += tree_sum<16>(a0);
-            s1 += tree_sum<16>(a1);
+            s0 += tree_sum<kBatch>(a0);
+            s1 += tree_sum<kBatch>(a1);
         }
         colsum[j][2 * q] = s0;
         colsum[j][2 * q + 1] = s1;
@@ -1354,14 +1389,14 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
             if (threadIdx.x >= 64 && threadIdx.x < 64 + 12)
                 sh_T64[threadIdx.x - 64] = __longlong_as_double(
                     (long long)ld_u64_sc1(is.T64 + (size_t)p * 16 + (threadIdx.x - 64)));
-            const double tsum = sum_pair_rows(rpart, is.nblk, colsum);
+            const double tsum = sum_pair_rows<8>(rpart, is.nblk, colsum);
             if (wave == 0) {
                 if (lane < kNeq) sh_neq[lane] = tsum;
                 if (is.stats && lane == 0) {
                     is.stats[((size_t)p * is.iters + k) * 2 + 0] = readlane64(tsum, 28);
                     is.stats[((size_t)p * is.iters + k) * 2 + 1] = readlane64(tsum, 27);
                 }
-                const int st = solve_update_wave(sh_neq, sh_T64, sh_T32n, sh_L, lane);
+                const int st = solve_update_wave_call(sh_neq, sh_T64, sh_T32n, sh_L, lane);
                 if (st && lane == 0)
                     __hip_atomic_fetch_or(is.status + p, st, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT);
@@ -1415,7 +1450,12 @@ constexpr int kCoopShards = 8;
 constexpr int kCoopShardStride = 32;  // words: one 128-B line per shard
 constexpr int kCoopMaxPx = 32;       // source pixels per lane (LDS: 3 x 32 KB)
 constexpr int kCoopMaxPairs = 16;     // counter words per set: 16 x 8 x 32
-constexpr int kCoopSetWords = kCoopMaxPairs * kCoopShards * kCoopShardStride + kCoopShardStride;
+// counter set layout (words): [pair][shard][32] arrivals | timeout word (one
+// line) | [pair][32] prep-done counters
+constexpr int kCoopErrWord = kCoopMaxPairs * kCoopShards * kCoopShardStride;
+constexpr int kCoopPrepWords = kCoopErrWord + kCoopShardStride;
+constexpr int kCoopSetWords = kCoopPrepWords + kCoopMaxPairs * kCoopShardStride;
+constexpr int kCoopTileH = 32;  // fused prep tiles: 64 x 32 pixels
 constexpr unsigned kCoopSpinMax = 1u << 22;  // polls (~1 us each): seconds, never reached
 
 struct CoopState {
@@ -1429,6 +1469,12 @@ struct CoopState {
     unsigned* set_next;    // the next call's: zeroed here
     unsigned* head_err;    // k_icp's queue words: error/telemetry cleared for get_poses
     int iters, n_pairs, G, npx;  // G workgroups per pair, npx source pixels per lane
+    // fused target prep (null: none): pair p's workgroups turn depth frame
+    // prep_src + p N into record frame prep_out0 + p; prep_wait: those are
+    // the records this launch gathers (hand-off before iteration 0), else
+    // they are for a later launch (the tracker's next reference frame)
+    const int16_t* prep_src;
+    int prep_out0, prep_wait, prep_wide;
 };
 
 // Phase timestamps for tools/coopbench only (never in the product build):
@@ -1551,6 +1597,9 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
                                                              CoopState cs)
 {
     extern __shared__ float coop_src[];  // [3][npx][kThreads]
+    __shared__ float sPX[(kCoopTileH + 2) * kLdsW];  // fused prep neighbourhood
+    __shared__ float sPY[(kCoopTileH + 2) * kLdsW];
+    __shared__ float sPZ[(kCoopTileH + 2) * kLdsW];
     __shared__ double red[kThreads / 64][kNeq];
     __shared__ double colsum[kSumCols][kPartStride];
     __shared__ double sh_neq[kNeq];
@@ -1566,7 +1615,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
     const int c = blockIdx.x - p * G;
     const int N = W * H;
     unsigned* cnt = cs.set + (size_t)p * kCoopShards * kCoopShardStride;
-    unsigned* err = cs.set + (size_t)kCoopMaxPairs * kCoopShards * kCoopShardStride;
+    unsigned* err = cs.set + kCoopErrWord;
+    unsigned* prep_cnt = cs.set + kCoopPrepWords + (size_t)p * kCoopShardStride;
     float* X = coop_src;
     float* Y = coop_src + npx * kThreads;
     float* Z = coop_src + 2 * npx * kThreads;
@@ -1584,6 +1634,30 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
                                    : ((threadIdx.x % 5) == 0 ? 1.0 : 0.0);
         sh_T64[threadIdx.x] = v;
         sh_T[threadIdx.x] = (float)v;
+    }
+    // ---- fused target prep: tiles c, c + G, ... of pair p's target frame,
+    // records stored write-through (sc1); every storing wave drains, then
+    // one arrival on the pair's prep counter (R1 hand-off)
+    if (cs.prep_src) {
+        const int tiles_x = (W + kTileW - 1) / kTileW;
+        const int tiles = tiles_x * ((H + kCoopTileH - 1) / kCoopTileH);
+        const int16_t* tdep = cs.prep_src + (size_t)p * N;
+        float4* R = const_cast<float4*>(recs) + (size_t)(cs.prep_out0 + p) * P;
+        for (int t = c; t < tiles; t += G) {  // uniform per workgroup
+            const int ty = t / tiles_x;
+            const int x0 = (t - ty * tiles_x) * kTileW, y0 = ty * kCoopTileH;
+            if (cs.prep_wide)
+                prep_tile<kFast, true, true, kThreads, kCoopTileH>(tdep, R, W, H, P, K, F, nullptr,
+                                                                   x0, y0, sPX, sPY, sPZ);
+            else
+                prep_tile<kFast, false, true, kThreads, kCoopTileH>(tdep, R, W, H, P, K, F,
+                                                                    nullptr, x0, y0, sPX, sPY, sPZ);
+            __syncthreads();  // LDS planes reused by the next tile
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
+        __syncthreads();
+        if (cs.prep_wait && threadIdx.x == 0)
+            __hip_atomic_fetch_add(prep_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // ---- this workgroup's source pixels, back-projected once (spec a2)
     {
@@ -1610,9 +1684,31 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
                                             : 0u;
     int32_t st_acc = 0;
     bool timeout = false;
-    __syncthreads();
+    if (cs.prep_src && cs.prep_wait) {
+        // every workgroup of pair p prepped its tiles: ONE relaxed poll, ONE
+        // agent acquire (drops this CU's stale L1 lines), then plain gathers
+        if (threadIdx.x == 0) {
+            unsigned spins = 0;
+            int stop = 0;
+            while (ld_u32_sc1(prep_cnt) < (unsigned)G) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > kCoopSpinMax || ld_u32_sc1(err) != 0u) {
+                    __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    stop = 1;
+                    break;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            sh_stop = stop;
+        }
+        __syncthreads();
+        timeout = __builtin_amdgcn_readfirstlane(sh_stop) != 0;
+    } else {
+        __syncthreads();
+    }
 
-    for (int k = 0; k < cs.iters; ++k) {
+    for (int k = 0; k < cs.iters && !timeout; ++k) {
         COOP_MARK(k, 0);
         float T[12];
 #pragma unroll
@@ -1688,7 +1784,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
         // ---- every workgroup sums the pair's partials in the same fixed order
         const __amdgpu_buffer_rsrc_t rpart = __builtin_amdgcn_make_buffer_rsrc(
             part, (short)0, G * kPartStride * (int)sizeof(double), 0x00020000);
-        const double tsum = sum_pair_rows(rpart, G, colsum);
+        const double tsum = sum_pair_rows<16>(rpart, G, colsum);
         COOP_MARK(k, 6);
         if (wave == 0) {
             if (lane < kNeq) sh_neq[lane] = tsum;
@@ -2028,8 +2124,18 @@ static const void* coop_kernel(bool fast, int threads)
     return fast ? (const void*)k_icp_coop<true, 512> : (const void*)k_icp_coop<false, 512>;
 }
 
+// Target frames to turn into records before (or, for the tracker, beside)
+// the iterations: depth frames [depth, depth + n N) -> record frames
+// [out0, out0 + n); wait: the iterations gather exactly these records.
+struct PrepJob {
+    const int16_t* depth;
+    int n, out0;
+    bool wait;
+};
+
 static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, PairMap pm,
-                       int n_pairs, const double* dTi, float* d_T_out, int npx, int G)
+                       int n_pairs, const double* dTi, float* d_T_out, int npx, int G,
+                       const PrepJob* job)
 {
     const int iters = c->prm.iters;
     int rc = ensure_partials(c, (size_t)2 * n_pairs * G * kPartStride);
@@ -2037,8 +2143,11 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
     unsigned* set = c->d_coop + (size_t)c->coop_par * kCoopSetWords;
     unsigned* set_next = c->d_coop + (size_t)(c->coop_par ^ 1) * kCoopSetWords;
     c->coop_par ^= 1;
-    CoopState cs{dTi, c->d_T64, c->d_T32, c->d_status, c->d_stats, d_T_out,
-                 set, set_next, c->d_head, iters, n_pairs, G, npx};
+    const bool wide = job && (c->W % 4 == 0) && (reinterpret_cast<uintptr_t>(job->depth) % 8 == 0);
+    CoopState cs{dTi,      c->d_T64, c->d_T32, c->d_status,          c->d_stats,
+                 d_T_out,  set,      set_next, c->d_head,            iters,
+                 n_pairs,  G,        npx,      job ? job->depth : nullptr,
+                 job ? job->out0 : 0, job && job->wait ? 1 : 0, wide ? 1 : 0};
     const float4* recs = c->d_rec;
     size_t P = c->P;
     int W = c->W, H = c->H;
@@ -2064,10 +2173,19 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
 // caller runs export_poses.
 static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, PairMap pm,
                           int n_pairs, const double* T_init_host, float* d_T_out = nullptr,
-                          bool* exported = nullptr)
+                          bool* exported = nullptr, const PrepJob* job = nullptr)
 {
     const int iters = c->prm.iters;
     if (exported) *exported = false;
+    // k_icp_coop fuses the prep job (one pair of workgroups per target);
+    // every other path runs k_prep first
+    int npx = 0, G = 0;
+    const bool coop = iters > 0 && (!job || job->n == n_pairs || (!job->wait && job->n == 1)) &&
+                      coop_plan(c, n_pairs, &npx, &G);
+    if (job && !coop) {
+        int rc = launch_prep(c, s, job->depth, job->n, job->out0, false);
+        if (rc) return rc;
+    }
     int rc = ensure_stats(c, iters > 0 ? iters : 1);
     if (rc) return rc;
     const double* dTi = nullptr;
@@ -2077,9 +2195,8 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
         dTi = c->d_Tinit;
     }
     {
-        int npx = 0, G = 0;
-        if (iters > 0 && coop_plan(c, n_pairs, &npx, &G)) {
-            rc = launch_coop(c, s, dsrc, pm, n_pairs, dTi, d_T_out, npx, G);
+        if (coop) {
+            rc = launch_coop(c, s, dsrc, pm, n_pairs, dTi, d_T_out, npx, G, job);
             if (rc) return rc;
             if (exported) *exported = d_T_out != nullptr;
             c->last_pairs = n_pairs;
@@ -2344,11 +2461,10 @@ int youth_icp_align_pairs_device(youth_icp_ctx* c, const int16_t* d_src, const i
     int rc = bind_device(c);
     if (rc) return rc;
     hipStream_t s = pick_stream(c, stream);
-    // targets -> records [0, n); sources are read from d_src by k_reduce
-    rc = launch_prep(c, s, d_dst, n_pairs, 0, false);
-    if (rc) return rc;
+    // targets -> records [0, n); sources are read straight from d_src
+    const PrepJob job{d_dst, n_pairs, 0, true};
     bool exported = false;
-    rc = run_iterations(c, s, d_src, PairMap{0, 0}, n_pairs, T_init, d_T_out, &exported);
+    rc = run_iterations(c, s, d_src, PairMap{0, 0}, n_pairs, T_init, d_T_out, &exported, &job);
     if (rc) return rc;
     return exported ? YOUTH_OK : export_poses(c, s, n_pairs, d_T_out);
 }
@@ -2361,12 +2477,12 @@ int youth_icp_align_sequence_device(youth_icp_ctx* c, const int16_t* d_frames, i
     int rc = bind_device(c);
     if (rc) return rc;
     hipStream_t s = pick_stream(c, stream);
-    // every frame but the last is a target: one record set per frame, reused
-    rc = launch_prep(c, s, d_frames, n_frames - 1, 0, false);
-    if (rc) return rc;
+    // every frame but the last is a target: one record set per frame, reused;
     // pair k: source depth frame k+1, target record frame k
+    const PrepJob job{d_frames, n_frames - 1, 0, true};
     bool exported = false;
-    rc = run_iterations(c, s, d_frames, PairMap{1, 0}, n_frames - 1, nullptr, d_T_out, &exported);
+    rc = run_iterations(c, s, d_frames, PairMap{1, 0}, n_frames - 1, nullptr, d_T_out, &exported,
+                        &job);
     if (rc) return rc;
     return exported ? YOUTH_OK : export_poses(c, s, n_frames - 1, d_T_out);
 }
@@ -2658,14 +2774,18 @@ int youth_icp_track_frame(youth_icp_ctx* c, const int16_t* depth, const double* 
     HIP_TRY(hipMemcpyAsync(c->d_depth + (size_t)slot * N, depth, N * sizeof(int16_t),
                            hipMemcpyHostToDevice, s));
     // the new frame is the next call's target: its records go to `slot`
-    rc = launch_prep(c, s, c->d_depth + (size_t)slot * N, 1, slot, false);
-    if (rc) return rc;
+    // (beside this call's iterations, which gather ref's records)
+    const PrepJob job{c->d_depth + (size_t)slot * N, 1, slot, false};
     int32_t st = 0;
     const int ref = c->track_ref;
     if (has_ref) *has_ref = ref >= 0;
-    if (ref >= 0) {
+    if (ref < 0) {
+        rc = launch_prep(c, s, job.depth, 1, slot, false);
+        if (rc) return rc;
+    } else {
         // source: the new frame's depth (staging slot); target: ref's records
-        rc = run_iterations(c, s, c->d_depth + (size_t)slot * N, PairMap{0, ref}, 1, T_init);
+        rc = run_iterations(c, s, c->d_depth + (size_t)slot * N, PairMap{0, ref}, 1, T_init,
+                            nullptr, nullptr, &job);
         if (rc) return rc;
         HIP_TRY(hipMemcpyAsync(T_rel, c->d_T64, 16 * sizeof(double), hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(&st, c->d_status, sizeof(int32_t), hipMemcpyDeviceToHost, s));

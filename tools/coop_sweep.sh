@@ -13,7 +13,7 @@ one() {  # label env... -- bench args
     python3 -c "import json,sys; d=json.loads(sys.argv[1]); k=d['kernel_ms_per_step']; print(f\"{sys.argv[2]:34s} {d['value']:9.0f} aligns/s  ms/step {d['ms_per_step']*1e3:7.1f} us  icp {k['k_reduce']*1e3:7.1f} us  prep {k['k_prep']*1e3:5.1f} us\")" "$out" "$label"
 }
 for r in $(seq 1 $R); do
-  for np in 1 2 4; do
+  for np in ${NPS:-1 2 4}; do
     S=$((200 / np + 20))
     one "pairs=$np persistent" YOUTH_ICP_NO_COOP=1 -- --pairs-per-gpu $np --steps $S --warmup 20 || exit 1
     one "pairs=$np coop planned 512" YOUTH_ICP_COOP_MAX_PAIRS=16 -- --pairs-per-gpu $np --steps $S --warmup 20 || exit 1
