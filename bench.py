@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpus)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-single-pair", action="store_true",
+                    help="skip the C2 leg (one pair per align call, rank 0, N=1)")
     ap.add_argument("--no-host-io", action="store_true",
                     help="skip the PCIe-inclusive host-buffer API leg (rank 0, N=1)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -183,12 +185,45 @@ def run_pairs(R):
     result["kernel_ms_per_step"] = {k: v[0] / a.steps for k, v in kt.items()}
     spins, waited = ctx.get_sched_stats()   # last align: persistent-kernel pose waits
     result["sched_last_step"] = {"epoch_polls": spins, "items_waited": waited}
+    result["kernel_path"] = ctx.get_plan()
     if rank == 0 and world == 1 and not a.no_host_io:
         result["host_io"] = host_io_rate(a, src, dst)
+    T_cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        result["cpu_baseline"], result["parity"] = cpu_baseline(a, src, dst, T_gpu)
+        result["cpu_baseline"], result["parity"], T_cpu = cpu_baseline(a, src, dst, T_gpu)
+    if rank == 0 and world == 1 and not a.no_single_pair and n > 1:
+        result["single_pair"] = single_pair_rate(R, d_src, d_dst, T_cpu)
     ctx.close()
     return result
+
+
+def single_pair_rate(R, d_src, d_dst, T_cpu, steps=400, warmup=40):
+    """BASELINE configs[1] (C2): ONE 640x480 pair per align call, calls back
+    to back on one stream (the latency path: processSlamFrame's tracker),
+    inputs resident in HBM.  Reported beside the C4-shard value, never as it;
+    the pose is checked against the C oracle's pose of the same pair."""
+    a = R.a
+    ctx = youth_icp.IcpContext(a.width, a.height, 2, iters=a.iters, device=R.local)
+    out = torch.zeros((1, 16), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    s0, t0p = d_src[0:1].data_ptr(), d_dst[0:1].data_ptr()
+    for _ in range(warmup):
+        ctx.align_pairs_device(s0, t0p, 1, d_T_out=out.data_ptr(), stream=stream)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.align_pairs_device(s0, t0p, 1, d_T_out=out.data_ptr(), stream=stream)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    T1, _, st = ctx.get_poses(1)
+    res = {"config": f"C2: one {a.width}x{a.height} pair per call, {a.iters} iters",
+           "value": steps / el, "unit": "aligns/s", "us_per_align": el / steps * 1e6,
+           "steps": steps, "warmup": warmup, "kernel_path": ctx.get_plan(),
+           "status": int(st[0])}
+    if T_cpu is not None:
+        res["pose_max_abs_err_vs_cpu"] = float(np.abs(T1[0, :3, :] - T_cpu[0, :3, :]).max())
+    ctx.close()
+    return res
 
 
 def run_sequence(R):
@@ -307,7 +342,7 @@ def cpu_baseline(a, src, dst, T_gpu):
            "host": {"cpu_model": model, "cpus_visible": cpus}}
     parity = {"pose_max_abs_err_vs_cpu": err, "pairs_checked": S, "tolerance": 1e-5,
               "cpu_status_nonzero": int((st != 0).sum())}
-    return cpu, parity
+    return cpu, parity, T_cpu
 
 
 def main():

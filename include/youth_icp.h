@@ -194,6 +194,13 @@ int youth_icp_get_timing(youth_icp_ctx* ctx, int kind, double* total_ms,
 int youth_icp_get_sched_stats(youth_icp_ctx* ctx, unsigned* spins,
                               unsigned* waited_items);
 
+/* Kernel path of the last align on this context (build-only, reporting):
+ * returns 1 when it ran the small-batch cooperative kernel (k_icp_coop:
+ * *workgroups_per_pair x 512 threads, *px_per_lane source pixels per lane,
+ * target prep fused), 0 for the persistent batch kernel (k_prep + k_icp),
+ * negative on error.  Either pointer may be NULL. */
+int youth_icp_get_plan(youth_icp_ctx* ctx, int* workgroups_per_pair, int* px_per_lane);
+
 /* Validation: compare the kernels' shared-reciprocal projection division with
  * IEEE fp32 a/b on n pseudo-random cases (seeded) on `device`.
  * *bit_mismatches counts bitwise differences where the IEEE expansion does not

@@ -1621,6 +1621,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
     float* Y = coop_src + npx * kThreads;
     float* Z = coop_src + 2 * npx * kThreads;
 
+    COOP_MARK(3, 15);  // prologue stamps: kernel entry (slot 15 of iterations 3, 0, 1, 2)
     if (blockIdx.x == 0) {
         for (int i = threadIdx.x; i < kCoopSetWords; i += kThreads) st_u32_sc1(cs.set_next + i, 0u);
         if (threadIdx.x == 0) {
@@ -1659,6 +1660,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
         if (cs.prep_wait && threadIdx.x == 0)
             __hip_atomic_fetch_add(prep_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    COOP_MARK(0, 15);  // prep published
     // ---- this workgroup's source pixels, back-projected once (spec a2)
     {
         const int16_t* sD = dsrc + (size_t)(pm.src0 + p) * N;
@@ -1684,6 +1686,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
                                             : 0u;
     int32_t st_acc = 0;
     bool timeout = false;
+    COOP_MARK(1, 15);  // source pixels staged
     if (cs.prep_src && cs.prep_wait) {
         // every workgroup of pair p prepped its tiles: ONE relaxed poll, ONE
         // agent acquire (drops this CU's stale L1 lines), then plain gathers
@@ -1708,6 +1711,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
         __syncthreads();
     }
 
+    COOP_MARK(2, 15);  // every record of the pair visible
     for (int k = 0; k < cs.iters && !timeout; ++k) {
         COOP_MARK(k, 0);
         float T[12];
@@ -1891,11 +1895,12 @@ struct youth_icp_ctx {
     bool coop = true;                // YOUTH_ICP_NO_COOP=1 disables
     int coop_px = 0;                 // YOUTH_ICP_COOP_PX: force pixels per lane (0: plan)
     int coop_threads = 512;          // YOUTH_ICP_COOP_THREADS=256: one wave per SIMD
-    int coop_max_pairs = 4;          // YOUTH_ICP_COOP_MAX_PAIRS (<= kCoopMaxPairs)
+    int coop_max_pairs = kCoopMaxPairs;  // YOUTH_ICP_COOP_MAX_PAIRS (<= kCoopMaxPairs)
     int coop_bpc[2][kCoopMaxPx + 1] = {};  // occupancy of k_icp_coop<fast> at npx (LDS)
     unsigned* d_coop = nullptr;      // 2 counter sets of kCoopSetWords
     int coop_par = 0;                // set used by the next coop call
     int last_coop_G = 0, last_coop_px = 0;
+    bool last_coop = false;          // the last align ran k_icp_coop
 
     int last_pairs = 0;
     int last_iters = 0;
@@ -2182,6 +2187,7 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
     int npx = 0, G = 0;
     const bool coop = iters > 0 && (!job || job->n == n_pairs || (!job->wait && job->n == 1)) &&
                       coop_plan(c, n_pairs, &npx, &G);
+    c->last_coop = coop;
     if (job && !coop) {
         int rc = launch_prep(c, s, job->depth, job->n, job->out0, false);
         if (rc) return rc;
@@ -2616,6 +2622,14 @@ int youth_icp_get_sched_stats(youth_icp_ctx* c, unsigned* spins, unsigned* waite
     if (spins) *spins = h[kQSpins];
     if (waited_items) *waited_items = h[kQWaited];
     return YOUTH_OK;
+}
+
+int youth_icp_get_plan(youth_icp_ctx* c, int* workgroups_per_pair, int* px_per_lane)
+{
+    if (!c) return set_error(YOUTH_EINVAL, "get_plan: null context");
+    if (workgroups_per_pair) *workgroups_per_pair = c->last_coop ? c->last_coop_G : 0;
+    if (px_per_lane) *px_per_lane = c->last_coop ? c->last_coop_px : 0;
+    return c->last_coop ? 1 : 0;
 }
 
 int youth_icp_get_timing(youth_icp_ctx* c, int kind, double* total_ms, int* launches)

@@ -98,6 +98,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "youth_icp_set_timing": (c_int, [c_void_p, c_int]),
         "youth_icp_get_timing": (c_int, [c_void_p, c_int, PD, POINTER(c_int)]),
         "youth_icp_get_sched_stats": (c_int, [c_void_p, POINTER(c_uint32), POINTER(c_uint32)]),
+        "youth_icp_get_plan": (c_int, [c_void_p, POINTER(c_int), POINTER(c_int)]),
         "youth_icp_selftest_projdiv": (c_int, [c_int, ctypes.c_longlong, ctypes.c_ulonglong,
                                                POINTER(ctypes.c_longlong),
                                                POINTER(ctypes.c_longlong)]),
@@ -361,6 +362,17 @@ class IcpContext:
         _check(self._lib.youth_icp_get_sched_stats(self._ctx, ctypes.byref(spins),
                                                    ctypes.byref(waited)))
         return spins.value, waited.value
+
+    def get_plan(self) -> dict:
+        """Kernel path of the last align: the small-batch cooperative kernel
+        (workgroups per pair, source pixels per lane) or the persistent one."""
+        g, px = c_int(0), c_int(0)
+        r = self._lib.youth_icp_get_plan(self._ctx, ctypes.byref(g), ctypes.byref(px))
+        _check(min(r, 0))
+        if r == 1:
+            return {"kernel": "k_icp_coop", "workgroups_per_pair": g.value, "threads": 512,
+                    "px_per_lane": px.value}
+        return {"kernel": "k_prep + k_icp (persistent)"}
 
     # host-array stage entry points (parity tests)
     def prepare(self, depth: np.ndarray, want_normals: bool = True):

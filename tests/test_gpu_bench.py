@@ -51,6 +51,10 @@ def test_bench_single_gpu_contract():
         assert k in cb, k
     assert cb["kind"] == "port" and cb["value"] > 0
     assert d["parity"]["pose_max_abs_err_vs_cpu"] <= 1e-5
+    sp = d["single_pair"]                   # C2 leg: one pair per call, small-batch kernel
+    assert sp["value"] > 0 and sp["status"] == 0 and sp["pose_max_abs_err_vs_cpu"] <= 1e-5
+    assert sp["kernel_path"]["kernel"] == "k_icp_coop"
+    assert d["kernel_path"]["kernel"].startswith("k_prep + k_icp")
 
 
 @pytest.mark.parametrize("workload", ["pairs", "sequence"])

@@ -70,7 +70,7 @@ int main(int argc, char** argv)
     CK(hipMemset(d_ph, 0, words * 8));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(coop_phase), &d_ph, sizeof(d_ph)));
     const int reps = 20;
-    std::vector<double> ph[8], hop, spread, total, sol[3], wv[4];
+    std::vector<double> ph[8], hop, spread, total, sol[3], wv[4], pro[6];
     std::vector<unsigned long long> h(words);
     for (int r = 0; r < reps; ++r) {
         if (youth_icp_align_pairs_device(c, d_s, d_d, n, nullptr, d_T, nullptr)) return 1;
@@ -105,6 +105,16 @@ int main(int argc, char** argv)
         }
         for (int p = 0; p < n; ++p)
             total.push_back((at(p * G, iters - 1, 7) - at(p * G, 1, 0)) * 10.0 / (iters - 1));
+        double t0 = 1e300;
+        for (int b = 0; b < blocks; ++b) t0 = std::min(t0, at(b, 3, 15));
+        for (int b = 0; b < blocks; ++b) {
+            pro[0].push_back((at(b, 3, 15) - t0) * 10.0);          // entry after first entry
+            pro[1].push_back((at(b, 0, 15) - at(b, 3, 15)) * 10.0);  // prep tiles
+            pro[2].push_back((at(b, 1, 15) - at(b, 0, 15)) * 10.0);  // source staging
+            pro[3].push_back((at(b, 2, 15) - at(b, 1, 15)) * 10.0);  // prep wait + acquire
+            pro[4].push_back((at(b, 0, 7) - at(b, 2, 15)) * 10.0);   // iteration 0
+            pro[5].push_back((at(b, iters - 1, 7) - t0) * 10.0);     // first entry -> last solve
+        }
     }
     const char* names[8] = {"pixel loop", "wg reduction", "publish+arrive", "poll (all arrived)",
                             "barrier", "sum partials", "solve+barrier", "loop back"};
@@ -122,6 +132,10 @@ int main(int argc, char** argv)
     printf("  %-22s %8.0f\n", "start spread", median(spread));
     printf("  wave 0 reduce-scatter %6.0f   pixel loop end of waves 1..3 - wave 0's: %6.0f %6.0f %6.0f\n",
            median(wv[0]), median(wv[1]), median(wv[2]), median(wv[3]));
+    printf("  prologue: entry skew %6.0f  prep %6.0f  source %6.0f  prep wait %6.0f  iteration 0 %6.0f"
+           "  entry->done %6.0f\n",
+           median(pro[0]), median(pro[1]), median(pro[2]), median(pro[3]), median(pro[4]),
+           median(pro[5]));
     printf("  chunk-0 lane 0: column sums -> solve %6.0f   LDL^T solve %6.0f   SE(3) exp %6.0f\n",
            median(sol[0]), median(sol[1]), median(sol[2]));
     youth_icp_destroy(c);
