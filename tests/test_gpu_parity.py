@@ -386,3 +386,36 @@ def test_plain_c_host_demo(tmp_path):
         T64, _, _, _ = oracle.align(frames[k], frames[k - 1])
         acc = acc @ T64
     assert np.allclose(rows[-1, 1:4], acc[:3, 3], atol=1e-6)
+
+
+@pytest.mark.parametrize("mode", ["coop", "persistent"])
+def test_kernel_paths_match_oracle(monkeypatch, mode):
+    """Both kernel paths of an align give the oracle's pose (<= 1e-5) and the
+    oracle's per-iteration correspondence counts, on repeated calls: the
+    small-batch cooperative kernel (k_icp_coop, fused prep) and the persistent
+    batch kernel (k_prep + k_icp)."""
+    if mode == "persistent":
+        monkeypatch.setenv("YOUTH_ICP_NO_COOP", "1")
+    n = 3
+    src, dst, _ = youth_synth.pairs(40, n)
+    import torch
+    ds = torch.from_numpy(src).cuda()
+    dd = torch.from_numpy(dst).cuda()
+    out = torch.zeros((n, 16), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    with youth_icp.IcpContext(640, 480, n) as ctx:
+        for _ in range(3):      # repeated calls: per-call state (counter sets, granules) re-armed
+            ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), n, d_T_out=out.data_ptr())
+        ctx.sync()
+        plan = ctx.get_plan()
+        T64, T32, st = ctx.get_poses(n)
+        cnt, _ = ctx.get_stats(n, 10)
+    assert plan["kernel"] == ("k_icp_coop" if mode == "coop" else
+                              "k_prep + k_icp (persistent)")
+    Tdev = out.cpu().numpy().reshape(n, 4, 4)
+    for p in range(n):
+        T64o, _, sto, stats = oracle.align(src[p], dst[p], iters=10)
+        assert st[p] == sto == 0
+        assert _pose_err(T64[p], T64o) <= POSE_TOL
+        assert np.array_equal(Tdev[p], T32[p])
+        assert np.array_equal(cnt[p], stats[:, 0])
