@@ -452,12 +452,54 @@ __device__ __forceinline__ void prep_tile(const int16_t* __restrict__ dep, float
     }
 }
 
+// The persistent path's per-call state, set by k_prep's tile-(0,0) blocks
+// (k_init's work folded in: one launch and its gap less per align): pair p's
+// T64/T32 from T_init (or identity), status 0, epoch 0, arrival tickets 0;
+// block (0,0,0) also zeroes the queue words.  n == 0: nothing.
+struct InitArgs {
+    const double* T_init;
+    int n;
+    double* T64;
+    float* T32;
+    int32_t* status;
+    unsigned* epoch;
+    unsigned* arrivals;  // [pair][iters]
+    int iters;
+    unsigned* head_err;
+};
+
+__device__ __forceinline__ void init_pairs(const InitArgs& ia)
+{
+    if (blockIdx.x != 0 || blockIdx.y != 0) return;
+    if (blockIdx.z == 0 && threadIdx.x == 0 && ia.head_err) {
+        ia.head_err[kQHead] = 0u;
+        ia.head_err[kQError] = 0u;
+        ia.head_err[kQSpins] = 0u;
+        ia.head_err[kQWaited] = 0u;
+    }
+    const int t = threadIdx.x;
+    for (int p = blockIdx.z; p < ia.n; p += gridDim.z) {
+        if (t < 16) {
+            const double v = ia.T_init ? ia.T_init[(size_t)p * 16 + t] : ((t % 5) == 0 ? 1.0 : 0.0);
+            ia.T64[(size_t)p * 16 + t] = v;
+            if (t < 12) ia.T32[(size_t)p * 12 + t] = (float)v;
+        } else if (t == 16) {
+            ia.status[p] = 0;
+            ia.epoch[p] = 0u;
+        } else {
+            for (int k = t - 17; k < ia.iters; k += kPrepThreads - 17)
+                ia.arrivals[(size_t)p * ia.iters + k] = 0u;
+        }
+    }
+}
+
 template <bool kFast, bool kWide>
 __global__ __launch_bounds__(kPrepThreads) void k_prep(const int16_t* __restrict__ depth, int out0,
                                                       int W, int H, size_t P, Intr K, FastK F,
                                                       float4* __restrict__ recs,
-                                                      float* __restrict__ xyz)
+                                                      float* __restrict__ xyz, InitArgs ia)
 {
+    init_pairs(ia);
     __shared__ float sX[kLdsH * kLdsW];
     __shared__ float sY[kLdsH * kLdsW];
     __shared__ float sZ[kLdsH * kLdsW];
@@ -1227,6 +1269,7 @@ struct IterState {
     unsigned* epoch;      // [pair], zeroed per call
     unsigned* head;       // dequeue counter, zeroed per call
     unsigned* error;      // timeout flag, zeroed per call
+    float* T_out;         // [pair][16] fp32 4x4 written by the final solve, or null
     int iters, n_pairs, nblk, chunk;
 };
 
@@ -1392,6 +1435,8 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
             const double tsum = sum_pair_rows<8>(rpart, is.nblk, colsum);
             if (wave == 0) {
                 if (lane < kNeq) sh_neq[lane] = tsum;
+                // the fp32 pose published when the solve skips the update (status != 0)
+                if (lane < 12) sh_T32n[lane] = (float)sh_T64[lane];
                 if (is.stats && lane == 0) {
                     is.stats[((size_t)p * is.iters + k) * 2 + 0] = readlane64(tsum, 28);
                     is.stats[((size_t)p * is.iters + k) * 2 + 1] = readlane64(tsum, 27);
@@ -1406,6 +1451,10 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
                                (unsigned long long)__double_as_longlong(sh_T64[lane]));
                     st_u32_sc1(is.T32 + (size_t)p * 12 + lane, __float_as_uint(sh_T32n[lane]));
                 }
+                // the pair's final pose as the fp32 4x4 output (k_finish folded in)
+                if (k == is.iters - 1 && is.T_out && lane < 16)
+                    is.T_out[(size_t)p * 16 + lane] =
+                        lane < 12 ? sh_T32n[lane] : (lane == 15 ? 1.0f : 0.0f);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 if (lane == 0) st_u32_sc1(is.epoch + p, (unsigned)(k + 1));
             }
@@ -2017,7 +2066,7 @@ static int ev_harvest(youth_icp_ctx* c)
 // Target records (and optionally XYZ planes) for n_frames depth frames at
 // `depth`, into workspace frames [out0, out0 + n_frames).
 static int launch_prep(youth_icp_ctx* c, hipStream_t s, const int16_t* depth, int n_frames,
-                       int out0, bool want_xyz)
+                       int out0, bool want_xyz, const InitArgs* init = nullptr)
 {
     if (n_frames <= 0) return YOUTH_OK;
     if (want_xyz) {
@@ -2032,8 +2081,9 @@ static int launch_prep(youth_icp_ctx* c, hipStream_t s, const int16_t* depth, in
     const bool wide = (c->W % 4 == 0) && (reinterpret_cast<uintptr_t>(depth) % 8 == 0);
     auto kern = c->fast ? (wide ? k_prep<true, true> : k_prep<true, false>)
                         : (wide ? k_prep<false, true> : k_prep<false, false>);
+    const InitArgs ia = init ? *init : InitArgs{};
     hipLaunchKernelGGL(kern, grid, dim3(kPrepThreads), 0, s, depth, out0, c->W, c->H, c->P, c->K,
-                       c->F, c->d_rec, xyz);
+                       c->F, c->d_rec, xyz, ia);
     HIP_TRY(hipGetLastError());
     return ev_end(c, s, &ep);
 }
@@ -2188,10 +2238,6 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
     const bool coop = iters > 0 && (!job || job->n == n_pairs || (!job->wait && job->n == 1)) &&
                       coop_plan(c, n_pairs, &npx, &G);
     c->last_coop = coop;
-    if (job && !coop) {
-        int rc = launch_prep(c, s, job->depth, job->n, job->out0, false);
-        if (rc) return rc;
-    }
     int rc = ensure_stats(c, iters > 0 ? iters : 1);
     if (rc) return rc;
     const double* dTi = nullptr;
@@ -2212,10 +2258,23 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
         }
     }
     const bool persistent = c->persistent && iters > 0;
-    hipLaunchKernelGGL(k_init, dim3((n_pairs + 63) / 64), dim3(64), 0, s, dTi, n_pairs, c->d_T64,
-                       c->d_T32, c->d_status, persistent ? c->d_epoch : (unsigned*)nullptr,
-                       persistent ? c->d_arr_it : (unsigned*)nullptr, iters, c->d_head);
-    HIP_TRY(hipGetLastError());
+    if (persistent && job) {
+        // k_prep also sets the per-call state (k_init folded in)
+        const InitArgs ia{dTi,         n_pairs,    c->d_T64, c->d_T32, c->d_status,
+                          c->d_epoch,  c->d_arr_it, iters,   c->d_head};
+        rc = launch_prep(c, s, job->depth, job->n, job->out0, false, &ia);
+        if (rc) return rc;
+    } else {
+        if (job) {
+            rc = launch_prep(c, s, job->depth, job->n, job->out0, false);
+            if (rc) return rc;
+        }
+        hipLaunchKernelGGL(k_init, dim3((n_pairs + 63) / 64), dim3(64), 0, s, dTi, n_pairs,
+                           c->d_T64, c->d_T32, c->d_status,
+                           persistent ? c->d_epoch : (unsigned*)nullptr,
+                           persistent ? c->d_arr_it : (unsigned*)nullptr, iters, c->d_head);
+        HIP_TRY(hipGetLastError());
+    }
     if (persistent) {
         int chunk = 0;
         const int nb = reduce_geometry(c, n_pairs, &chunk);
@@ -2227,8 +2286,11 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
         long long grid = (long long)c->n_cu * c->icp_blocks_per_cu[var];
         if (grid > items) grid = items;
         if (grid < 1) grid = 1;
-        const IterState is{c->d_T64, c->d_T32, c->d_status, c->d_stats, c->d_arr_it, c->d_epoch,
-                           c->d_head + kQHead, c->d_head + kQError, iters, n_pairs, nb, chunk};
+        const IterState is{c->d_T64,  c->d_T32,  c->d_status, c->d_stats,
+                           c->d_arr_it, c->d_epoch, c->d_head + kQHead, c->d_head + kQError,
+                           d_T_out,   iters,      n_pairs,    nb,
+                           chunk};
+        if (exported) *exported = d_T_out != nullptr;  // k_icp's final solves write d_T_out
         const float thr2 = c->prm.dist_thresh * c->prm.dist_thresh;
         EventPair ep{};
         rc = ev_begin(c, s, &ep, 0);
@@ -2518,10 +2580,17 @@ int youth_icp_get_poses(youth_icp_ctx* c, int n, double* T64, float* T32, int32_
         HIP_TRY(hipMemcpyAsync(T32, c->d_Tout, (size_t)n * 16 * sizeof(float),
                                hipMemcpyDeviceToHost, s));
     }
-    if (status)
+    unsigned err = 0;
+    if (status) {
         HIP_TRY(hipMemcpyAsync(status, c->d_status, (size_t)n * sizeof(int32_t),
                                hipMemcpyDeviceToHost, s));
+        // a timed-out launch (either kernel path) marks every pair
+        HIP_TRY(hipMemcpyAsync(&err, c->d_head + kQError, sizeof(unsigned),
+                               hipMemcpyDeviceToHost, s));
+    }
     HIP_TRY(hipStreamSynchronize(s));
+    if (status && err)
+        for (int i = 0; i < n; ++i) status[i] |= YOUTH_STATUS_TIMEOUT;
     return YOUTH_OK;
 }
 

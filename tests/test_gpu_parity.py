@@ -419,3 +419,36 @@ def test_kernel_paths_match_oracle(monkeypatch, mode):
         assert _pose_err(T64[p], T64o) <= POSE_TOL
         assert np.array_equal(Tdev[p], T32[p])
         assert np.array_equal(cnt[p], stats[:, 0])
+
+
+@pytest.mark.parametrize("mode", ["coop", "persistent"])
+def test_kernel_paths_skipped_update(monkeypatch, mode):
+    """A pair whose every iteration skips the update (no valid source pixels:
+    YOUTH_STATUS_FEW_MATCHES) keeps its initial pose in T64, T32 and the fp32
+    output on both kernel paths, while its batch neighbours converge."""
+    if mode == "persistent":
+        monkeypatch.setenv("YOUTH_ICP_NO_COOP", "1")
+    n = 3
+    src, dst, _ = youth_synth.pairs(50, n)
+    src[1] = 0
+    import torch
+    ds = torch.from_numpy(src).cuda()
+    dd = torch.from_numpy(dst).cuda()
+    out = torch.full((n, 16), 7.0, dtype=torch.float32, device="cuda")
+    T_init = np.tile(np.eye(4), (n, 1, 1))
+    T_init[1, :3, 3] = [0.25, -0.5, 0.125]
+    torch.cuda.synchronize()
+    with youth_icp.IcpContext(640, 480, n) as ctx:
+        ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), n, T_init=T_init,
+                               d_T_out=out.data_ptr())
+        ctx.sync()
+        T64, T32, st = ctx.get_poses(n)
+    Tdev = out.cpu().numpy().reshape(n, 4, 4)
+    assert st[1] == youth_icp.STATUS_FEW_MATCHES
+    assert np.array_equal(T64[1], T_init[1])
+    assert np.array_equal(T32[1], T_init[1].astype(np.float32))
+    assert np.array_equal(Tdev[1], T_init[1].astype(np.float32))
+    for p in (0, 2):
+        T64o, _, sto, _ = oracle.align(src[p], dst[p], iters=10, T_init=T_init[p])
+        assert st[p] == sto == 0 and _pose_err(T64[p], T64o) <= POSE_TOL
+        assert np.array_equal(Tdev[p], T32[p])
