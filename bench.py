@@ -94,13 +94,23 @@ class Run:
         for _ in range(a.warmup):
             step()
         self.barrier_sync()
-        ctx.set_timing(True)
+        # events around the iteration kernel only inside the timed region (the
+        # roofline's launch durations); every kernel kind in a short pass after it
+        ctx.set_timing(True, iteration_kernel_only=True)
         t0 = time.perf_counter()
         for _ in range(a.steps):
             step()
         self.barrier_sync()
         elapsed = time.perf_counter() - t0
-        kt = {k: ctx.get_timing(i) for i, k in enumerate(("k_reduce", "k_solve", "k_prep"))}
+        kt = {"k_reduce": ctx.get_timing(0)}
+        ctx.set_timing(True)
+        extra = min(a.steps, 5)
+        for _ in range(extra):
+            step()
+        self.barrier_sync()
+        for i, k in ((1, "k_solve"), (2, "k_prep")):
+            ms, cnt = ctx.get_timing(i)
+            kt[k] = (ms * a.steps / extra, cnt)   # scaled to the timed region's step count
         ctx.set_timing(False)
         if self.world > 1:
             dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
@@ -161,17 +171,32 @@ def run_pairs(R):
     src, dst, _ = youth_synth.pairs(first, cnt, W, H)
     d_src = torch.from_numpy(src).cuda()
     d_dst = torch.from_numpy(dst).cuda()
-    poses = torch.zeros((n, 16), dtype=torch.float32, device="cuda")
+    # double-buffered poses: the RCCL gather of step s runs on its own stream
+    # while step s+1 aligns; step s+2 waits for it before reusing the buffers
+    # (every gather completes inside the timed region: final device sync)
+    poses = [torch.zeros((n, 16), dtype=torch.float32, device="cuda") for _ in range(2)]
+    gathered = [torch.zeros((world * n, 16), dtype=torch.float32, device="cuda")
+                for _ in range(2)]
+    pending = [None, None]
     ctx = youth_icp.IcpContext(W, H, max(n, 2), iters=a.iters, device=R.local)
     stream = torch.cuda.current_stream().cuda_stream
+    it = [0]
 
     def step():
+        b = it[0] & 1
+        it[0] += 1
+        if pending[b] is not None:
+            pending[b].wait()
         ctx.align_pairs_device(d_src.data_ptr(), d_dst.data_ptr(), n,
-                               d_T_out=poses.data_ptr(), stream=stream)
-        youth_dist.gather_poses(poses, world)
+                               d_T_out=poses[b].data_ptr(), stream=stream)
+        pending[b] = youth_dist.gather_poses_async(poses[b], gathered[b], world)
 
     elapsed, kt = R.timed(ctx, step)
     T_gpu, _, _ = ctx.get_poses(n)          # fp64 poses of the last step
+    lb = (it[0] - 1) & 1                     # the last step's gathered poses: every rank's
+    if world > 1 and not np.array_equal(gathered[lb][R.rank * n:(R.rank + 1) * n].cpu().numpy(),
+                                        poses[lb].cpu().numpy()):
+        raise RuntimeError("pose all-gather: this rank's rows differ from its poses")
     result = base_result(R, world * n * a.steps / elapsed, elapsed)
     result["scaling"] = "weak"
     result["config"] = {
@@ -205,7 +230,11 @@ def single_pair_rate(R, d_src, d_dst, T_cpu, steps=400, warmup=40):
     a = R.a
     ctx = youth_icp.IcpContext(a.width, a.height, 2, iters=a.iters, device=R.local)
     out = torch.zeros((1, 16), dtype=torch.float32, device="cuda")
-    stream = torch.cuda.current_stream().cuda_stream
+    # the library's own (non-blocking) stream: nothing in torch consumes `out`
+    # before the final synchronize.  (Cooperative launches on the bench's torch
+    # stream ran at half this rate inside this process, 4.5 K vs 9.1 K aligns/s,
+    # though not in a standalone probe: tools/stream_probe.py)
+    stream = 0
     s0, t0p = d_src[0:1].data_ptr(), d_dst[0:1].data_ptr()
     for _ in range(warmup):
         ctx.align_pairs_device(s0, t0p, 1, d_T_out=out.data_ptr(), stream=stream)
@@ -238,13 +267,15 @@ def run_sequence(R):
     ctx = youth_icp.IcpContext(W, H, max(npairs, 2), iters=a.iters, device=R.local)
     stream = torch.cuda.current_stream().cuda_stream
     max_rows = (F - 1 + world - 1) // world
+    counts = [max(0, (lambda f: f[1] - f[0] - 1)(youth_dist.sequence_shard(F, world, r)))
+              for r in range(world)]
     traj = {}
 
     def step():
         if npairs:
             ctx.align_sequence_device(d_frames.data_ptr(), nf, d_T_out=rel.data_ptr(),
                                       stream=stream)
-        rows = youth_dist.gather_ragged(rel[:npairs], world, max_rows)
+        rows = youth_dist.gather_ragged(rel[:npairs], world, max_rows, counts)
         if rank == 0:
             traj["T"] = rows   # composed after the timed region (host, ordered fp64)
 
@@ -348,7 +379,12 @@ def cpu_baseline(a, src, dst, T_gpu):
 def main():
     a = parse()
     R = Run(a)
-    result = run_pairs(R) if a.workload == "pairs" else run_sequence(R)
+    # a non-default torch stream: its handle is what every align is issued on,
+    # so the pose copies and the RCCL gathers (which wait on torch's current
+    # stream) are ordered after the kernels that write the poses (handle 0 would
+    # select the library's private stream instead)
+    with torch.cuda.stream(torch.cuda.Stream()):
+        result = run_pairs(R) if a.workload == "pairs" else run_sequence(R)
     if R.rank == 0:
         print(json.dumps(result), flush=True)
     R.finish()

@@ -180,8 +180,10 @@ int youth_icp_get_poses(youth_icp_ctx* ctx, int n, double* T64, float* T32,
 int youth_icp_get_stats(youth_icp_ctx* ctx, int n, int iters, double* count,
                         double* sum_r2);
 
-/* Kernel timing (HIP events on the launch stream around every normal-equation
- * reduction launch; for bench.py's roofline).  enable=1 resets counters. */
+/* Kernel timing (HIP events on the launch stream; for bench.py's roofline).
+ * enable=1: around every iteration-kernel launch (kind 0), solve (1) and prep
+ * (2) launch; enable=2: around the iteration kernel only (fewer markers in a
+ * timed region); 0: off.  Any call resets the counters. */
 int youth_icp_set_timing(youth_icp_ctx* ctx, int enable);
 /* total_ms / launches of reduction (kind 0), solve (1), frame-prep (2). */
 int youth_icp_get_timing(youth_icp_ctx* ctx, int kind, double* total_ms,

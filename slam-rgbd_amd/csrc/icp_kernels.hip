@@ -1958,6 +1958,7 @@ struct youth_icp_ctx {
     int track_ref = -1;  // ring slot (0/1) of the tracker's reference frame
 
     bool timing = false;
+    bool timing_iter_only = false;  // set_timing(2): events around the iteration kernel only
     std::vector<EventPair> ev_live;
     std::vector<EventPair> ev_free;
     double t_ms[3] = {0, 0, 0};
@@ -2027,7 +2028,8 @@ static int ensure_xyz(youth_icp_ctx* c)
 
 static int ev_begin(youth_icp_ctx* c, hipStream_t s, EventPair* ep, int kind)
 {
-    if (!c->timing) return YOUTH_OK;
+    ep->a = nullptr;
+    if (!c->timing || (c->timing_iter_only && kind != 0)) return YOUTH_OK;
     if (c->ev_free.empty()) {
         EventPair e{};
         HIP_TRY(hipEventCreate(&e.a));
@@ -2043,7 +2045,7 @@ static int ev_begin(youth_icp_ctx* c, hipStream_t s, EventPair* ep, int kind)
 
 static int ev_end(youth_icp_ctx* c, hipStream_t s, EventPair* ep)
 {
-    if (!c->timing) return YOUTH_OK;
+    if (!c->timing || !ep->a) return YOUTH_OK;
     HIP_TRY(hipEventRecord(ep->b, s));
     c->ev_live.push_back(*ep);
     return YOUTH_OK;
@@ -2620,6 +2622,7 @@ int youth_icp_set_timing(youth_icp_ctx* c, int enable)
     rc = ev_harvest(c);
     if (rc) return rc;
     c->timing = enable != 0;
+    c->timing_iter_only = enable == 2;
     for (int k = 0; k < 3; ++k) {
         c->t_ms[k] = 0.0;
         c->t_n[k] = 0;

@@ -52,18 +52,37 @@ def gather_poses(local: torch.Tensor, world: int) -> torch.Tensor:
     return out
 
 
-def gather_ragged(local: torch.Tensor, world: int, max_rows: int) -> torch.Tensor:
+def gather_poses_async(local: torch.Tensor, out: torch.Tensor, world: int):
+    """Start the all-gather of [n, 16] pose rows into `out` ([world * n, 16],
+    rank-ordered) and return its work handle (RCCL: `handle.wait()` makes the
+    current stream wait for it, the host does not block), or None when there
+    is nothing to wait for (world 1: no gather, `out` untouched; gloo: host
+    tensors, synchronous).
+    Callers double-buffer `local` / `out` so the next align overlaps the
+    gather of the previous one."""
+    if world == 1:
+        return None   # nothing to gather: `out` is not written
+    if dist.get_backend() == "nccl":
+        return dist.all_gather_into_tensor(out, local.contiguous(), async_op=True)
+    out.copy_(gather_poses(local, world))
+    return None
+
+
+def gather_ragged(local: torch.Tensor, world: int, max_rows: int,
+                  counts: list[int] | None = None) -> torch.Tensor:
     """All-gather [m_r, 16] rows with different m_r per rank (sequence
-    shards): pad to max_rows, gather counts and rows, strip padding."""
+    shards): pad to max_rows, gather the rows (and the counts, unless the
+    caller knows them: sequence_shard gives every rank's), strip padding."""
     if world == 1:
         return local
     pad = torch.zeros((max_rows,) + tuple(local.shape[1:]), dtype=local.dtype,
                       device=local.device)
     pad[: local.shape[0]] = local
-    cnt = torch.tensor([local.shape[0]], dtype=torch.int64, device=local.device)
-    counts = gather_poses(cnt, world)
+    if counts is None:
+        cnt = torch.tensor([local.shape[0]], dtype=torch.int64, device=local.device)
+        counts = [int(v) for v in gather_poses(cnt, world)]
     rows = gather_poses(pad, world).view(world, max_rows, *local.shape[1:])
-    return torch.cat([rows[r, : int(counts[r])] for r in range(world)])
+    return torch.cat([rows[r, : counts[r]] for r in range(world)])
 
 
 def compose_trajectory(rel: np.ndarray) -> np.ndarray:

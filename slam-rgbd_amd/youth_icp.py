@@ -347,8 +347,11 @@ class IcpContext:
                                              _p(r2, c_double)))
         return cnt, r2
 
-    def set_timing(self, enable: bool) -> None:
-        _check(self._lib.youth_icp_set_timing(self._ctx, 1 if enable else 0))
+    def set_timing(self, enable, iteration_kernel_only: bool = False) -> None:
+        """HIP-event timing of the launches (every kernel kind, or only the
+        iteration kernel: fewer markers inside a timed region)."""
+        mode = (2 if iteration_kernel_only else 1) if enable else 0
+        _check(self._lib.youth_icp_set_timing(self._ctx, mode))
 
     def get_timing(self, kind: int = 0):
         ms, n = c_double(0.0), c_int(0)

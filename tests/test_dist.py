@@ -35,11 +35,20 @@ def _worker(rank, world, port, q):
         src, dst, T_gt = youth_synth.pairs(first, cnt, 64, 48)
         local = torch.from_numpy(T_gt.reshape(cnt, 16).astype(np.float32))
         allp = youth_dist.gather_poses(local, world)
+        out = torch.zeros((world * cnt, 16), dtype=torch.float32)
+        h = youth_dist.gather_poses_async(local, out, world)   # bench.py's double-buffered form
+        if h is not None:
+            h.wait()
+        assert torch.equal(out, allp)
         # sequence: 9 frames -> 8 pairs over 2 ranks with a 1-frame halo
         f0, f1 = youth_dist.sequence_shard(9, world, rank)
         frames, Twc = youth_synth.sequence(f0, f1 - f0, 64, 48)
         rel = np.stack([np.linalg.inv(Twc[k]) @ Twc[k + 1] for k in range(f1 - f0 - 1)])
         rows = youth_dist.gather_ragged(torch.from_numpy(rel.reshape(-1, 16)), world, 8)
+        counts = [max(0, (lambda f: f[1] - f[0] - 1)(youth_dist.sequence_shard(9, world, r)))
+                  for r in range(world)]
+        rows_k = youth_dist.gather_ragged(torch.from_numpy(rel.reshape(-1, 16)), world, 8, counts)
+        assert torch.equal(rows, rows_k)
         q.put((rank, allp.numpy(), (f0, f1), rows.numpy()))
     finally:
         dist.destroy_process_group()
