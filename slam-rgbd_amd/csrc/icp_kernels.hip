@@ -2248,16 +2248,22 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
                                hipMemcpyHostToDevice, s));
         dTi = c->d_Tinit;
     }
-    {
-        if (coop) {
-            rc = launch_coop(c, s, dsrc, pm, n_pairs, dTi, d_T_out, npx, G, job);
-            if (rc) return rc;
+    if (coop) {
+        rc = launch_coop(c, s, dsrc, pm, n_pairs, dTi, d_T_out, npx, G, job);
+        if (rc == YOUTH_OK) {
             if (exported) *exported = d_T_out != nullptr;
             c->last_pairs = n_pairs;
             c->last_iters = iters;
             c->last_stream = s;
             return YOUTH_OK;
         }
+        // the runtime refused the cooperative launch (nothing was enqueued): this
+        // context takes the persistent path from now on
+        fprintf(stderr, "youth_icp: cooperative launch refused (%s); using the persistent path\n",
+                youth_icp_last_error());
+        (void)hipGetLastError();
+        c->coop = false;
+        c->last_coop = false;
     }
     const bool persistent = c->persistent && iters > 0;
     if (persistent && job) {
