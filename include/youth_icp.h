@@ -155,7 +155,10 @@ void youth_icp_destroy(youth_icp_ctx* ctx);
  * unmodified until the align has completed on `stream`).  T_init: nullable HOST [n_pairs][16] fp64 (identity
  * if NULL).  d_T_out: nullable DEVICE [n_pairs][16] fp32.  stream: a
  * hipStream_t as void* (NULL = the context's own stream).  Asynchronous:
- * returns after enqueueing; use youth_icp_sync / youth_icp_get_poses. */
+ * returns after enqueueing; use youth_icp_sync / youth_icp_get_poses.  One
+ * context's aligns must execute in order (one stream, or ordered by the
+ * caller): they share its workspace and per-call hand-off state.  Small
+ * batches run as one cooperative launch (youth_icp_get_plan). */
 int youth_icp_align_pairs_device(youth_icp_ctx* ctx, const int16_t* d_src,
                                  const int16_t* d_dst, int n_pairs,
                                  const double* T_init, float* d_T_out,
