@@ -58,7 +58,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(16, cpus)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single-pair", action="store_true",
-                    help="skip the C2 leg (one pair per align call, rank 0, N=1)")
+                    help="skip the C2 leg (one pair per align call) / the streamed sequence leg "
+                         "(rank 0, N=1)")
     ap.add_argument("--no-host-io", action="store_true",
                     help="skip the PCIe-inclusive host-buffer API leg (rank 0, N=1)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -292,8 +293,37 @@ def run_sequence(R):
     if rank == 0:
         T = youth_dist.compose_trajectory(traj["T"].cpu().numpy().reshape(-1, 4, 4))
         result["trajectory_frames"] = int(T.shape[0])
+        if world == 1 and not a.no_single_pair:
+            result["streamed"] = streamed_rate(a, frames, rel[:npairs].cpu().numpy())
     ctx.close()
     return result
+
+
+def streamed_rate(a, frames, rel_batch, n=300):
+    """The same sequence streamed frame by frame from HOST memory through the
+    tracker (youth_icp_track_frame: processSlamFrame's path): per frame one
+    614 KB H2D, target prep of the new frame + 10 iterations against the
+    previous one (one k_icp_coop launch), pose D2H, synchronous.  Reported
+    beside the batch value; relative poses checked against the batch run's."""
+    n = min(n, frames.shape[0])
+    ctx = youth_icp.IcpContext(a.width, a.height, 2, iters=a.iters)
+    ctx.track_frame(frames[0])
+    ctx.track_frame(frames[1])                         # warm
+    ctx.track_reset()
+    t0 = time.perf_counter()
+    rel = []
+    for f in range(n):
+        T, st, has = ctx.track_frame(frames[f])
+        if has:
+            rel.append(T)
+    el = time.perf_counter() - t0
+    plan = ctx.get_plan()
+    ctx.close()
+    rel = np.stack(rel)
+    err = float(np.abs(rel[:, :3, :] - rel_batch[: n - 1].reshape(-1, 4, 4)[:, :3, :]).max())
+    return {"frames": n, "value": n / el, "unit": "frames/s", "us_per_frame": el / n * 1e6,
+            "kernel_path": plan, "max_abs_diff_vs_batch_poses": err,
+            "note": "host frames, H2D + align + pose D2H per frame, synchronous"}
 
 
 def base_result(R, value, elapsed):
