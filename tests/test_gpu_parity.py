@@ -452,3 +452,19 @@ def test_kernel_paths_skipped_update(monkeypatch, mode):
         T64o, _, sto, _ = oracle.align(src[p], dst[p], iters=10, T_init=T_init[p])
         assert st[p] == sto == 0 and _pose_err(T64[p], T64o) <= POSE_TOL
         assert np.array_equal(Tdev[p], T32[p])
+
+
+def test_max_frame_size_8192x8192():
+    """The largest frame youth_icp_create accepts (W*H = 2^26): 24-bit index
+    multiply, 32-bit record byte offsets and the persistent path (one pair is
+    too large for the cooperative kernel) at full size.  Pose within 1e-5 of
+    the oracle; association at the final pose bit-exact over all 67 M pixels."""
+    W = H = 8192
+    K = youth_icp.default_intrinsics(W, H)
+    src, dst, _ = youth_synth.pairs(7, 1, W, H)
+    Tg, assoc = youth_icp.align_batch(src, dst, K=K, iters=2, want_assoc=True)
+    T64, _, st, _ = oracle.align(src[0], dst[0], K, iters=2)
+    assert st == 0 and _pose_err(Tg[0], T64) <= POSE_TOL
+    idx = oracle.associate(src[0], dst[0], Tg[0][:3], K)
+    assert int((idx >= 0).sum()) > W * H // 4
+    assert np.array_equal(assoc[0], idx)
