@@ -37,6 +37,7 @@ import numpy as np  # noqa: E402
 import youth_dist  # noqa: E402
 import youth_icp  # noqa: E402
 import youth_synth  # noqa: E402
+import youth_viewer  # noqa: E402
 
 METRIC = "ICP frame-pair aligns/sec @640×480 (1/2/4/8 GPU); SE(3) err vs CPU ref"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
@@ -60,6 +61,8 @@ def parse():
     ap.add_argument("--no-single-pair", action="store_true",
                     help="skip the C2 leg (one pair per align call) / the streamed sequence leg "
                          "(rank 0, N=1)")
+    ap.add_argument("--no-viewer", action="store_true",
+                    help="skip the viewer point-list leg (SURVEY §8 f4; rank 0, N=1)")
     ap.add_argument("--no-host-io", action="store_true",
                     help="skip the PCIe-inclusive host-buffer API leg (rank 0, N=1)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -219,6 +222,8 @@ def run_pairs(R):
         result["cpu_baseline"], result["parity"], T_cpu = cpu_baseline(a, src, dst, T_gpu)
     if rank == 0 and world == 1 and not a.no_single_pair and n > 1:
         result["single_pair"] = single_pair_rate(R, d_src, d_dst, T_cpu)
+    if rank == 0 and world == 1 and not a.no_viewer:
+        result["viewer_cloud"] = viewer_cloud_rate(R, d_dst, dst)
     ctx.close()
     return result
 
@@ -253,6 +258,60 @@ def single_pair_rate(R, d_src, d_dst, T_cpu, steps=400, warmup=40):
     if T_cpu is not None:
         res["pose_max_abs_err_vs_cpu"] = float(np.abs(T1[0, :3, :] - T_cpu[0, :3, :]).max())
     ctx.close()
+    return res
+
+
+def viewer_cloud_rate(R, d_depth, depth_host, reps=20, warmup=3):
+    """the viewer's vertex list (viewerModule.c:336-357) for the
+    rank's n frames in one device call (youth_cloud_build_device: count, scan,
+    emit), synthetic RGB, inputs resident in HBM; HIP events on the launching
+    stream.  Algorithmic bytes: 2 B depth + 3 B colour per pixel read, 24 B
+    per vertex written.  Frame 0's list is checked bit-exact against the C
+    oracle (oracle_viewer_cloud)."""
+    a = R.a
+    n, H, W = depth_host.shape
+    rgb = np.random.default_rng(0xC0105).integers(0, 256, size=(n, H, W, 3), dtype=np.uint8)
+    d_rgb = torch.from_numpy(rgb).cuda()
+    verts = torch.empty((n, H * W, 6), dtype=torch.float32, device="cuda")
+    counts = torch.zeros(n, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream()
+    cb = youth_viewer.CloudBuilder(W, H, max_frames=n, device=R.local)
+
+    def call():
+        cb.build_device(d_depth.data_ptr(), d_rgb.data_ptr(), n, W, H, verts.data_ptr(),
+                        counts.data_ptr(), stream=s.cuda_stream)
+
+    for _ in range(warmup):
+        call()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        call()
+    e1.record(s)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    cnt = counts.cpu().numpy()
+    nbytes = float(n * H * W * 5 + int(cnt.sum()) * 24)
+    res = {"frames_per_call": n, "width": W, "height": H, "us_per_call": ms * 1e3,
+           "value": n / (ms * 1e-3), "unit": "frames/s",
+           "vertices_per_frame": float(cnt.mean()),
+           "roofline": {"bound": "hbm", "achieved": nbytes / (ms * 1e-3) / 1e9,
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                        "algorithmic_bytes_per_call": nbytes,
+                        "kernels": "k_cloud_count + k_cloud_scan + k_cloud_emit"}}
+    if not a.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        want = oracle.viewer_cloud(depth_host[0], rgb[0])
+        got = verts[0, : int(cnt[0])].cpu().numpy()
+        res["bit_exact_vs_cpu"] = bool(got.shape == want.shape and
+                                       np.array_equal(got.view(np.uint32), want.view(np.uint32)))
+        t0 = time.perf_counter()
+        for f in range(min(n, 8)):
+            oracle.viewer_cloud(depth_host[f], rgb[f])
+        res["cpu_frames_per_s_1thread"] = min(n, 8) / (time.perf_counter() - t0)
+    cb.close()
     return res
 
 

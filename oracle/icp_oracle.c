@@ -365,3 +365,31 @@ int oracle_max_threads(void)
     return 1;
 #endif
 }
+
+/* viewerModule.c:336-357 (display_3d_color's loop), minus the GL calls: the
+ * glColor3f / glVertex3f arguments of every valid pixel, in loop order. */
+int oracle_viewer_cloud(const int16_t* depth, const uint8_t* rgb, int W, int H,
+                        const oracle_intrinsics* K, float* vertices)
+{
+    int n = 0;
+    for (int y = 0; y < H; ++y) {
+        for (int x = 0; x < W; ++x) {
+            const int index = y * W + x;
+            const int d = depth[index];
+            if (d > 0) {
+                const float z = (float)d / K->depth_scale;
+                const float xp = (((float)x - K->cx) * z) / K->fx;
+                const float yp = (((float)y - K->cy) * z) / K->fy;
+                float* o = vertices + (size_t)n * 6;
+                o[0] = -xp;
+                o[1] = -yp;
+                o[2] = -z;
+                o[3] = rgb ? (float)rgb[(size_t)index * 3 + 0] / 255.0f : 0.0f;
+                o[4] = rgb ? (float)rgb[(size_t)index * 3 + 1] / 255.0f : 0.0f;
+                o[5] = rgb ? (float)rgb[(size_t)index * 3 + 2] / 255.0f : 0.0f;
+                ++n;
+            }
+        }
+    }
+    return n;
+}

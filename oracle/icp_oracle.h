@@ -96,6 +96,15 @@ void oracle_align_batch(const int16_t* src, const int16_t* dst, int n_pairs,
 /* Threads OpenMP will use for n_threads <= 0 (1 when built without OpenMP). */
 int oracle_max_threads(void);
 
+/* Viewer point list: the vertices display_3d_color emits,
+ * Youth.Source/ViewerModule/viewerModule.c:336-357.  Raster order, valid
+ * pixels (d > 0) only; vertex k = {-x, -y, -z, r, g, b} (6 floats) with
+ * x, y, z the back-projection above (viewerModule.c:343-345, K = the viewer
+ * convention reproduces it bit-for-bit) and r, g, b = rgb[3i+c] / 255.0f
+ * (:349-352).  rgb may be NULL (colour 0).  Returns the vertex count. */
+int oracle_viewer_cloud(const int16_t* depth, const uint8_t* rgb, int W, int H,
+                        const oracle_intrinsics* K, float* vertices);
+
 #ifdef __cplusplus
 }
 #endif

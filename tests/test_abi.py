@@ -16,6 +16,7 @@ from conftest import GOLDEN, PKG, ROOT
 HEADERS = {
     "youth_icp.h": os.path.join(PKG, "libyouth_icp.so"),
     "youth_wire.h": os.path.join(PKG, "libyouth_icp.so"),
+    "youth_viewer.h": os.path.join(PKG, "libyouth_icp.so"),
     "youth_synth.h": os.path.join(PKG, "libyouth_synth.so"),
 }
 
@@ -83,6 +84,11 @@ def test_no_device_fails_loudly(has_gpu):
     assert youth_icp.getSlamMapPoints() == 0
     lib = youth_icp.load_library()
     assert lib.algorithmModule(None) is None     # returns instead of hanging
+    # viewer point list (youth_viewer.h): no builder without a device
+    import youth_viewer
+    with pytest.raises(youth_icp.IcpError) as e:
+        youth_viewer.CloudBuilder(64, 48)
+    assert e.value.code == youth_icp.YOUTH_ENODEV
 
 
 def test_queue_overflow_policy_matches_reference():

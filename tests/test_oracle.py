@@ -169,3 +169,52 @@ def test_batch_openmp_matches_single():
     for p in range(4):
         T64, _, s1, _ = oracle.align(src[p], dst[p], iters=5)
         assert np.array_equal(Tb[p], T64) and st[p] == s1
+
+
+def _viewer_loop_numpy(depth, rgb):
+    """viewerModule.c:336-357 restated in numpy fp32 (one IEEE rounding per
+    operation, as the C source evaluates it): the glVertex3f(-x,-y,-z) and
+    glColor3f(r,g,b) arguments of every pixel with depth > 0, loop order."""
+    H, W = depth.shape
+    d = depth.astype(np.int32)
+    u = np.arange(W, dtype=np.int32)[None, :].repeat(H, 0)
+    v = np.arange(H, dtype=np.int32)[:, None].repeat(W, 1)
+    z = d.astype(np.float32) / np.float32(1000.0)
+    x = (u - W // 2).astype(np.float32) * z / np.float32(570.3)
+    y = (v - H // 2).astype(np.float32) * z / np.float32(570.3)
+    col = rgb.astype(np.float32) / np.float32(255.0)
+    valid = (d > 0).reshape(-1)   # raster order == the loop's y-major, x-minor order
+    out = np.stack([-x.reshape(-1), -y.reshape(-1), -z.reshape(-1),
+                    col[..., 0].reshape(-1), col[..., 1].reshape(-1), col[..., 2].reshape(-1)], 1)
+    return out[valid].astype(np.float32)
+
+
+@pytest.mark.parametrize("W,H", [(64, 48), (97, 53), (5, 7), (1, 9)])
+def test_viewer_cloud_matches_viewer_loop(W, H):
+    """The oracle's viewer point list equals the reference
+    loop restated in numpy, bit for bit, including -0.0 on the centre column."""
+    rng = np.random.default_rng(W * 1000 + H)
+    depth = rng.integers(-300, 32768, size=(H, W)).astype(np.int16)
+    depth[rng.random((H, W)) < 0.2] = 0
+    rgb = rng.integers(0, 256, size=(H, W, 3)).astype(np.uint8)
+    got = oracle.viewer_cloud(depth, rgb)
+    want = _viewer_loop_numpy(depth, rgb)
+    assert got.shape == want.shape
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    # no colour buffer: colour 0, same geometry
+    g0 = oracle.viewer_cloud(depth, None)
+    assert np.array_equal(g0[:, :3].view(np.uint32), want[:, :3].view(np.uint32))
+    assert not g0[:, 3:].any()
+
+
+def test_viewer_cloud_pinned_to_kat():
+    """Each KAT pixel (SURVEY.md §4 bit patterns of viewerModule.c:343-345)
+    comes out as the single vertex (-x, -y, -z)."""
+    table = _load("kat_backproject")["table"]
+    for W, H, u, v, d, xb, yb, zb in table.tolist():
+        depth = np.zeros((H, W), np.int16)
+        depth[v, u] = d
+        vert = oracle.viewer_cloud(depth)
+        assert vert.shape == (1, 6)
+        neg = (-vert[0, :3]).astype(np.float32)
+        assert tuple(int(b) for b in neg.view(np.uint32)) == (xb, yb, zb)
