@@ -24,6 +24,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -32,35 +33,70 @@
 namespace {
 
 constexpr int kCloudThreads = 256;
-constexpr int kCloudPx = 8;                              // pixels per thread
-constexpr int kCloudTile = kCloudThreads * kCloudPx;     // 2048 pixels per workgroup
 constexpr int kVF = YOUTH_CLOUD_FLOATS_PER_VERTEX;      // 6 floats per vertex
 
 struct CloudK {
     float fx, fy, cx, cy, ds;
 };
 
-// 8 depth values of pixels [i, i+8) of one frame; kVec: one 16-byte load
-// (frame base 16-B aligned, N % 8 == 0, so i + 8 <= N whenever i < N).
-template <bool kVec>
-__device__ __forceinline__ void load_depth8(const int16_t* __restrict__ d, int i, int N, int dd[8])
+// kPx depth values of pixels [i, i+kPx) of one frame.  kVec: one 8-/16-byte
+// load (frame base aligned, N % kPx == 0, so i + kPx <= N whenever i < N).
+template <bool kVec, int kPx>
+__device__ __forceinline__ void load_depth(const int16_t* __restrict__ d, int i, int N, int* dd)
 {
     if (kVec) {
+        int v[kPx / 2];
         if (i < N) {
-            const int4 w = *reinterpret_cast<const int4*>(d + i);
-            const int v[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                dd[2 * k] = (int)(short)(v[k] & 0xffff);   // little-endian: low half first
-                dd[2 * k + 1] = v[k] >> 16;                // arithmetic shift: sign kept
+            if constexpr (kPx == 8) {
+                const int4 w = *reinterpret_cast<const int4*>(d + i);
+                v[0] = w.x;
+                v[1] = w.y;
+                v[2] = w.z;
+                v[3] = w.w;
+            } else {
+                const int2 w = *reinterpret_cast<const int2*>(d + i);
+                v[0] = w.x; v[1] = w.y;
             }
         } else {
 #pragma unroll
-            for (int k = 0; k < 8; ++k) dd[k] = 0;
+            for (int k = 0; k < kPx / 2; ++k) v[k] = 0;
+        }
+#pragma unroll
+        for (int k = 0; k < kPx / 2; ++k) {
+            dd[2 * k] = (int)(short)(v[k] & 0xffff);   // little-endian: low half first
+            dd[2 * k + 1] = v[k] >> 16;                // arithmetic shift: sign kept
         }
     } else {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) dd[k] = (i + k) < N ? (int)d[i + k] : 0;
+        for (int k = 0; k < kPx; ++k) dd[k] = (i + k) < N ? (int)d[i + k] : 0;
+    }
+}
+
+// kPx * 3 colour bytes of pixels [i, i+kPx) (viewerModule.c:348-352): kVec
+// loads 8-byte (kPx 8) or 4-byte (kPx 4) words, the offset (fN + i) * 3
+// being a multiple of 24 / 12.
+template <bool kVec, int kPx>
+__device__ __forceinline__ void load_rgb(const uint8_t* __restrict__ c, int i, int N,
+                                         unsigned char* cc)
+{
+    if (kVec && i < N) {
+        unsigned wds[kPx * 3 / 4];
+        if constexpr (kPx == 8) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const uint2 w = *reinterpret_cast<const uint2*>(c + 8 * k);
+                wds[2 * k] = w.x;
+                wds[2 * k + 1] = w.y;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) wds[k] = *reinterpret_cast<const unsigned*>(c + 4 * k);
+        }
+#pragma unroll
+        for (int k = 0; k < kPx * 3; ++k) cc[k] = (unsigned char)(wds[k >> 2] >> (8 * (k & 3)));
+    } else {
+#pragma unroll
+        for (int k = 0; k < kPx * 3; ++k) cc[k] = (i + k / 3) < N ? c[k] : (unsigned char)0;
     }
 }
 
@@ -82,19 +118,19 @@ __device__ __forceinline__ int wave_incl_scan_i32(int x, int lane)
     return x;
 }
 
-template <bool kVec>
+template <bool kVec, int kPx>
 __global__ __launch_bounds__(kCloudThreads) void k_cloud_count(const int16_t* __restrict__ depth,
                                                                 int N, int tiles,
                                                                 int32_t* __restrict__ tile_cnt)
 {
     __shared__ int sw[kCloudThreads / 64];
     const int f = blockIdx.y, tile = blockIdx.x;
-    const int i = tile * kCloudTile + threadIdx.x * kCloudPx;
-    int dd[8];
-    load_depth8<kVec>(depth + (size_t)f * N, i, N, dd);
+    const int i = (tile * kCloudThreads + threadIdx.x) * kPx;
+    int dd[kPx];
+    load_depth<kVec, kPx>(depth + (size_t)f * N, i, N, dd);
     int c = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) c += dd[k] > 0 ? 1 : 0;   // viewerModule.c:342
+    for (int k = 0; k < kPx; ++k) c += dd[k] > 0 ? 1 : 0;   // viewerModule.c:342
     c = wave_sum_i32(c);
     if ((threadIdx.x & 63) == 0) sw[threadIdx.x >> 6] = c;
     __syncthreads();
@@ -136,40 +172,36 @@ __global__ __launch_bounds__(kCloudThreads) void k_cloud_scan(const int32_t* __r
     if (threadIdx.x == kCloudThreads - 1) counts[f] = woff + incl;
 }
 
-template <bool kVec>
+// The tile's vertices are staged in LDS in list order, placed so that LDS
+// float j and output float (run start - head + j) share their offset mod 4
+// (head = the run start's float offset within its 16-byte granule); the run
+// is then copied out in 16-byte stores, element stores only for the partial
+// granules at its two ends.  (Storing each vertex straight from registers,
+// 3 x 8-byte stores, measured 1.7x slower: 64 lanes' partial lines per
+// instruction; profiles/r01/cloud_ab.txt.)
+template <bool kVec, int kPx>
 __global__ __launch_bounds__(kCloudThreads) void k_cloud_emit(
     const int16_t* __restrict__ depth, const uint8_t* __restrict__ rgb, int W, int N, int tiles,
     CloudK K, const int32_t* __restrict__ tile_off, float* __restrict__ vertices)
 {
-    __shared__ float stage[kCloudTile * kVF];   // 48 KB: the tile's vertices in list order
+    constexpr int kTile = kCloudThreads * kPx;
+    __shared__ __align__(16) float stage[kTile * kVF + 4];   // the tile's vertices, list order
     __shared__ int sw[kCloudThreads / 64];
     const int f = blockIdx.y, tile = blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int i = tile * kCloudTile + threadIdx.x * kCloudPx;
-    int dd[8];
-    load_depth8<kVec>(depth + (size_t)f * N, i, N, dd);
-    // colour of the 8 pixels: 24 bytes at (f N + i) * 3 (viewerModule.c:348-352)
-    unsigned char cc[24];
+    const int i = (tile * kCloudThreads + threadIdx.x) * kPx;
+    int dd[kPx];
+    load_depth<kVec, kPx>(depth + (size_t)f * N, i, N, dd);
+    unsigned char cc[kPx * 3];
     if (rgb) {
-        const uint8_t* c = rgb + ((size_t)f * N + i) * 3;
-        if (kVec && i < N) {
-            const uint2 a = *reinterpret_cast<const uint2*>(c);
-            const uint2 b = *reinterpret_cast<const uint2*>(c + 8);
-            const uint2 e = *reinterpret_cast<const uint2*>(c + 16);
-            const unsigned wds[6] = {a.x, a.y, b.x, b.y, e.x, e.y};
-#pragma unroll
-            for (int k = 0; k < 24; ++k) cc[k] = (unsigned char)(wds[k >> 2] >> (8 * (k & 3)));
-        } else {
-#pragma unroll
-            for (int k = 0; k < 24; ++k) cc[k] = (i + k / 3) < N ? c[k] : (unsigned char)0;
-        }
+        load_rgb<kVec, kPx>(rgb + ((size_t)f * N + i) * 3, i, N, cc);
     } else {
 #pragma unroll
-        for (int k = 0; k < 24; ++k) cc[k] = 0;
+        for (int k = 0; k < kPx * 3; ++k) cc[k] = 0;
     }
     int c = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) c += dd[k] > 0 ? 1 : 0;
+    for (int k = 0; k < kPx; ++k) c += dd[k] > 0 ? 1 : 0;
     const int incl = wave_incl_scan_i32(c, lane);
     if (lane == 63) sw[wave] = incl;
     __syncthreads();
@@ -180,23 +212,23 @@ __global__ __launch_bounds__(kCloudThreads) void k_cloud_emit(
         total += sw[w];
     }
     int slot = woff + incl - c;
-    // (u, v) of pixel i; a thread's 8 pixels may wrap rows (any W >= 1)
+    float* out = vertices + ((size_t)f * N + (size_t)tile_off[(size_t)f * tiles + tile]) * kVF;
+    const int head = (int)(((uintptr_t)out >> 2) & 3);
+    // (u, v) of pixel i; a thread's pixels may wrap rows (any W >= 1)
     int v = i / W;
     int u = i - v * W;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < kPx; ++k) {
         if (dd[k] > 0) {
             // viewerModule.c:343-345, evaluated as written (IEEE quotients)
             const float z = (float)dd[k] / K.ds;
             const float x = (((float)u - K.cx) * z) / K.fx;
             const float y = (((float)v - K.cy) * z) / K.fy;
-            float* o = stage + slot * kVF;
-            o[0] = -x;   // glVertex3f(-x_pos, -y_pos, -z_pos), :354
-            o[1] = -y;
-            o[2] = -z;
-            o[3] = (float)cc[3 * k + 0] / 255.0f;   // :349-351
-            o[4] = (float)cc[3 * k + 1] / 255.0f;
-            o[5] = (float)cc[3 * k + 2] / 255.0f;
+            // glVertex3f(-x_pos, -y_pos, -z_pos) (:354), glColor3f(r, g, b) (:349-351)
+            const float o[kVF] = {-x, -y, -z, (float)cc[3 * k + 0] / 255.0f,
+                                  (float)cc[3 * k + 1] / 255.0f, (float)cc[3 * k + 2] / 255.0f};
+#pragma unroll
+            for (int q = 0; q < kVF; ++q) stage[head + slot * kVF + q] = o[q];
             ++slot;
         }
         ++u;
@@ -206,10 +238,21 @@ __global__ __launch_bounds__(kCloudThreads) void k_cloud_emit(
         }
     }
     __syncthreads();
-    // the tile's run of the frame's list: contiguous, written in order
-    float* out = vertices + ((size_t)f * N + (size_t)tile_off[(size_t)f * tiles + tile]) * kVF;
+    // the tile's run of the frame's list, floats [head, head + nf) of the
+    // 16-byte granules starting at out - head
     const int nf = total * kVF;
-    for (int k = threadIdx.x; k < nf; k += kCloudThreads) out[k] = stage[k];
+    const int end = head + nf;
+    float* base = out - head;
+    for (int g = threadIdx.x; g * 4 < end; g += kCloudThreads) {
+        const int j = g * 4;
+        if (j >= head && j + 4 <= end) {
+            *reinterpret_cast<float4*>(base + j) = *reinterpret_cast<const float4*>(stage + j);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (j + q >= head && j + q < end) base[j + q] = stage[j + q];
+        }
+    }
 }
 
 }  // namespace
@@ -239,6 +282,7 @@ __attribute__((format(printf, 2, 3))) static int cloud_error(int code, const cha
 struct youth_cloud_ctx {
     int device = 0;
     int W = 0, H = 0, N = 0, max_frames = 0, max_tiles = 0;
+    int px = 8;   // pixels per thread (tile = 256 px): YOUTH_CLOUD_PX=4|8
     hipStream_t stream = nullptr;
     int32_t* d_tile_cnt = nullptr;   // [max_frames][max_tiles]
     int32_t* d_tile_off = nullptr;   // [max_frames][max_tiles]
@@ -292,7 +336,8 @@ youth_cloud_ctx* youth_cloud_create(int device, int W, int H, int max_frames)
     c->H = H;
     c->N = W * H;
     c->max_frames = max_frames;
-    c->max_tiles = (c->N + kCloudTile - 1) / kCloudTile;
+    if (const char* e = getenv("YOUTH_CLOUD_PX")) c->px = atoi(e) == 4 ? 4 : 8;
+    c->max_tiles = (c->N + kCloudThreads * 4 - 1) / (kCloudThreads * 4);   // room for px = 4
     const size_t nt = (size_t)max_frames * c->max_tiles;
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -326,26 +371,31 @@ int youth_cloud_build_device(youth_cloud_ctx* c, const int16_t* d_depth, const u
     if (n_frames == 0) return YOUTH_OK;
     CLOUD_TRY(hipSetDevice(c->device));
     const int N = W * H;
-    const int tiles = (N + kCloudTile - 1) / kCloudTile;
+    const int tile_px = kCloudThreads * c->px;
+    const int tiles = (N + tile_px - 1) / tile_px;
     CloudK k{570.3f, 570.3f, (float)(W / 2), (float)(H / 2), 1000.0f};   // viewerModule.c:343-345
     if (K) k = CloudK{K->fx, K->fy, K->cx, K->cy, K->depth_scale};
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    const bool vec = (N % 8) == 0 && ((uintptr_t)d_depth % 16) == 0 &&
-                     (!d_rgb || ((uintptr_t)d_rgb % 8) == 0);
+    // vector loads: every frame base and thread offset aligned for the
+    // 2 px-byte depth word and the 3 px-byte colour words
+    const bool vec = (N % c->px) == 0 && ((uintptr_t)d_depth % (2 * c->px)) == 0 &&
+                     (!d_rgb || ((uintptr_t)d_rgb % (c->px == 8 ? 8 : 4)) == 0);
+    using CountFn = void (*)(const int16_t*, int, int, int32_t*);
+    using EmitFn = void (*)(const int16_t*, const uint8_t*, int, int, int, CloudK, const int32_t*,
+                            float*);
+    static const CountFn count_fn[2][2] = {{k_cloud_count<false, 4>, k_cloud_count<true, 4>},
+                                           {k_cloud_count<false, 8>, k_cloud_count<true, 8>}};
+    static const EmitFn emit_fn[2][2] = {{k_cloud_emit<false, 4>, k_cloud_emit<true, 4>},
+                                         {k_cloud_emit<false, 8>, k_cloud_emit<true, 8>}};
+    const int pi = c->px == 8 ? 1 : 0;
     const dim3 grid(tiles, n_frames);
-    if (vec)
-        k_cloud_count<true><<<grid, kCloudThreads, 0, s>>>(d_depth, N, tiles, c->d_tile_cnt);
-    else
-        k_cloud_count<false><<<grid, kCloudThreads, 0, s>>>(d_depth, N, tiles, c->d_tile_cnt);
+    hipLaunchKernelGGL(count_fn[pi][vec], grid, dim3(kCloudThreads), 0, s, d_depth, N, tiles,
+                       c->d_tile_cnt);
     CLOUD_TRY(hipGetLastError());
     k_cloud_scan<<<n_frames, kCloudThreads, 0, s>>>(c->d_tile_cnt, tiles, c->d_tile_off, d_counts);
     CLOUD_TRY(hipGetLastError());
-    if (vec)
-        k_cloud_emit<true><<<grid, kCloudThreads, 0, s>>>(d_depth, d_rgb, W, N, tiles, k,
-                                                          c->d_tile_off, d_vertices);
-    else
-        k_cloud_emit<false><<<grid, kCloudThreads, 0, s>>>(d_depth, d_rgb, W, N, tiles, k,
-                                                           c->d_tile_off, d_vertices);
+    hipLaunchKernelGGL(emit_fn[pi][vec], grid, dim3(kCloudThreads), 0, s, d_depth,
+                       d_rgb, W, N, tiles, k, (const int32_t*)c->d_tile_off, d_vertices);
     CLOUD_TRY(hipGetLastError());
     return YOUTH_OK;
 }

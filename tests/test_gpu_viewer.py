@@ -77,10 +77,13 @@ def test_cloud_explicit_intrinsics():
     assert np.array_equal(_bits(got), _bits(want))
 
 
+@pytest.mark.parametrize("px", [8, 4])
 @pytest.mark.parametrize("offset", [0, 1])
-def test_cloud_device_batch(offset):
+def test_cloud_device_batch(offset, px, monkeypatch):
     """Device API over a stacked batch on a torch stream; offset 1 misaligns the
-    depth/colour pointers (scalar-load path)."""
+    depth/colour pointers (scalar-load path) and the output run alignment; both
+    tile widths (pixels per thread, read at builder creation)."""
+    monkeypatch.setenv("YOUTH_CLOUD_PX", str(px))
     W, H, n = 320, 240, 5
     frames = [_frame(W, H, 100 + f) for f in range(n)]
     d_all = torch.zeros(n * H * W + offset, dtype=torch.int16, device="cuda")
