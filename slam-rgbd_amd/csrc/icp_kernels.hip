@@ -36,6 +36,8 @@
 
 #include <mutex>
 #include <string>
+#include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "youth_icp.h"
@@ -1957,6 +1959,10 @@ struct youth_icp_ctx {
 
     int track_ref = -1;  // ring slot (0/1) of the tracker's reference frame
 
+    // host-buffer batch API: H2D of chunk k+1 on xfer overlaps the align of chunk k
+    hipStream_t xfer = nullptr;
+    std::vector<hipEvent_t> xfer_ev;
+
     bool timing = false;
     bool timing_iter_only = false;  // set_timing(2): events around the iteration kernel only
     std::vector<EventPair> ev_live;
@@ -2404,6 +2410,8 @@ void youth_icp_destroy(youth_icp_ctx* c)
             (void)hipEventDestroy(e.a);
             (void)hipEventDestroy(e.b);
         }
+    if (c->xfer) (void)hipStreamSynchronize(c->xfer);
+    for (hipEvent_t e : c->xfer_ev) (void)hipEventDestroy(e);
     void* bufs[] = {c->d_depth, c->d_rec,   c->d_xyz,      c->d_T64, c->d_T32,   c->d_status,
                     c->d_Tinit, c->d_stats, c->d_partials, c->d_neq, c->d_assoc, c->d_Tout,
                     c->d_flag,  c->d_arrivals, c->d_arr_it, c->d_epoch, c->d_head,
@@ -2411,6 +2419,7 @@ void youth_icp_destroy(youth_icp_ctx* c)
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->xfer) (void)hipStreamDestroy(c->xfer);
     delete c;
 }
 
@@ -2804,6 +2813,18 @@ int youth_icp_solve_host(youth_icp_ctx* c, const double* neq, double* T64)
 static std::mutex g_batch_mu;
 static youth_icp_ctx* g_batch_ctx = nullptr;
 
+// Pairs per pipelined chunk of the host-buffer batch API (n_pairs: no
+// pipelining).  YOUTH_ICP_BATCH_CHUNK overrides (0 disables).
+static int batch_chunk(int n_pairs, size_t N)
+{
+    if (const char* e = getenv("YOUTH_ICP_BATCH_CHUNK")) {
+        const int v = atoi(e);
+        return v <= 0 ? n_pairs : std::min(v, n_pairs);
+    }
+    (void)N;
+    return n_pairs >= 16 ? 8 : n_pairs;   // 8 pairs: copy ~ align (profiles/r01/hostio_sweep.txt)
+}
+
 int youth_icp_align_batch(const int16_t* src, const int16_t* dst, int n_pairs, int W, int H,
                           const youth_intrinsics* K, int iters, float* T_out,
                           int32_t* assoc_out)
@@ -2834,6 +2855,37 @@ int youth_icp_align_batch(const int16_t* src, const int16_t* dst, int n_pairs, i
     const size_t N = c->N;
     int16_t* d_s = c->d_depth;
     int16_t* d_d = c->d_depth + (size_t)n_pairs * N;
+    const int chunk = assoc_out ? n_pairs : batch_chunk(n_pairs, N);
+    if (chunk < n_pairs) {
+        // pipelined: chunk k's depth goes up on the transfer stream while the
+        // align of chunk k-1 runs on the compute stream (every chunk has its
+        // own device frames, so no buffer is reused inside one call)
+        if (!c->xfer) HIP_TRY(hipStreamCreateWithFlags(&c->xfer, hipStreamNonBlocking));
+        const int n_chunks = (n_pairs + chunk - 1) / chunk;
+        while ((int)c->xfer_ev.size() < n_chunks) {
+            hipEvent_t e;
+            HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            c->xfer_ev.push_back(e);
+        }
+        for (int k = 0; k < n_chunks; ++k) {
+            const size_t p0 = (size_t)k * chunk;
+            const int cnt = (int)std::min<size_t>(chunk, n_pairs - p0);
+            const size_t bytes = (size_t)cnt * N * sizeof(int16_t);
+            HIP_TRY(hipMemcpyAsync(d_s + p0 * N, src + p0 * N, bytes, hipMemcpyHostToDevice,
+                                   c->xfer));
+            HIP_TRY(hipMemcpyAsync(d_d + p0 * N, dst + p0 * N, bytes, hipMemcpyHostToDevice,
+                                   c->xfer));
+            HIP_TRY(hipEventRecord(c->xfer_ev[k], c->xfer));
+            HIP_TRY(hipStreamWaitEvent(s, c->xfer_ev[k], 0));
+            rc = youth_icp_align_pairs_device(c, d_s + p0 * N, d_d + p0 * N, cnt, nullptr,
+                                              c->d_Tout + p0 * 16, s);
+            if (rc) return rc;
+        }
+        HIP_TRY(hipMemcpyAsync(T_out, c->d_Tout, (size_t)n_pairs * 16 * sizeof(float),
+                               hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        return YOUTH_OK;
+    }
     HIP_TRY(hipMemcpyAsync(d_s, src, (size_t)n_pairs * N * sizeof(int16_t), hipMemcpyHostToDevice,
                            s));
     HIP_TRY(hipMemcpyAsync(d_d, dst, (size_t)n_pairs * N * sizeof(int16_t), hipMemcpyHostToDevice,

@@ -149,6 +149,23 @@ def test_align_batch_640x480_matches_oracle():
         assert np.array_equal(assoc[p], oracle.associate(src[p], dst[p], Tg[p][:3]))
 
 
+@pytest.mark.parametrize("chunk", ["0", "8", "5"])
+def test_align_batch_pipelined_chunks(chunk, monkeypatch):
+    """Host-buffer batch API with H2D of chunk k+1 overlapping the align of
+    chunk k (YOUTH_ICP_BATCH_CHUNK; 21 pairs leaves a ragged last chunk):
+    poses within tolerance of the oracle and of the unpipelined call."""
+    n = 21
+    src, dst, _ = youth_synth.pairs(100, n, 160, 120)
+    monkeypatch.setenv("YOUTH_ICP_BATCH_CHUNK", "0")
+    T_one, _ = youth_icp.align_batch(src, dst, iters=10)
+    monkeypatch.setenv("YOUTH_ICP_BATCH_CHUNK", chunk)
+    T_chk, _ = youth_icp.align_batch(src, dst, iters=10)
+    assert float(np.abs(T_chk - T_one).max()) <= 1e-12
+    for p in (0, 7, 8, 20):
+        T64, _, st, _ = oracle.align(src[p], dst[p], iters=10)
+        assert _pose_err(T_chk[p], T64) <= POSE_TOL, p
+
+
 def test_context_device_api_poses_and_stats():
     n = 6
     src, dst, _ = youth_synth.pairs(20, n)
