@@ -408,7 +408,7 @@ def host_io_rate(a, src, dst, reps=5):
     """PCIe-inclusive rate of the one-shot host API (youth_icp_align_batch):
     H2D of both depth stacks + align + D2H of the poses, synchronous, from
     pageable (numpy) and pinned (torch pin_memory) host buffers; the H2D of
-    chunk k+1 overlaps the align of chunk k (8-pair chunks).  Reported beside
+    chunk k+1 overlaps the align of chunk k (16-pair chunks).  Reported beside
     the bench value, never as it (inputs there are resident in HBM)."""
     out = {"api": "youth_icp_align_batch", "pairs": int(src.shape[0]),
            "h2d_bytes_per_pair": int(2 * src[0].nbytes)}

@@ -2822,7 +2822,10 @@ static int batch_chunk(int n_pairs, size_t N)
         return v <= 0 ? n_pairs : std::min(v, n_pairs);
     }
     (void)N;
-    return n_pairs >= 16 ? 8 : n_pairs;   // 8 pairs: copy ~ align (profiles/r01/hostio_sweep.txt)
+    // 16-pair chunks run the persistent kernel: copy ~ align.  8-pair chunks
+    // (cooperative kernel) ran at 34 K on one box and 20-24 K on another, next to
+    // the in-flight copies (profiles/r01/hostio_sweep.txt)
+    return n_pairs >= 32 ? 16 : n_pairs;
 }
 
 int youth_icp_align_batch(const int16_t* src, const int16_t* dst, int n_pairs, int W, int H,
