@@ -19,7 +19,8 @@
  *   back-projection does, youth_icp.h), r,g,b = rgb[3 index + c] / 255.0f
  *   (:349-352; rgb NULL gives colour 0).
  *
- * Plain C99, no HIP or torch types (streams travel as void*).  Entry points
+ * A context is used by one thread at a time; its device calls on one stream
+ * run in order.  Plain C99, no HIP or torch types (streams travel as void*).  Entry points
  * return YOUTH_OK (0) / a count >= 0, or a negative YOUTH_E* code
  * (youth_icp.h); the text of the last error is youth_cloud_last_error().
  */

@@ -166,6 +166,46 @@ def test_align_batch_pipelined_chunks(chunk, monkeypatch):
         assert _pose_err(T_chk[p], T64) <= POSE_TOL, p
 
 
+@pytest.mark.parametrize("n", [1, 40])
+def test_large_step_rodrigues_branch(n):
+    """Spec a10 above theta = 5 deg (theta^2 >= 2^-7): the SE(3) update leaves
+    the Taylor form for sqrt/sincos (OCML on the GPU, libm in the oracle: may
+    differ in an ulp).  T_init is 7 deg off the true motion and the gate is
+    opened to 1 m, so the Gauss-Newton step is ~8 deg; one iteration (from
+    there projective ICP leaves its basin, and a chaotic trajectory is no
+    parity case), both kernel paths (n = 1: cooperative, n = 40: persistent);
+    pose within the north-star tolerance, and the wave solve's large-angle
+    branch also through the single-lane solve entry point."""
+    import torch  # plumbing only: device memory
+    W, H = 320, 240
+    src, dst, Tgt = youth_synth.pairs(300, n, W, H)
+    axis = np.array([0.3, 1.0, 0.2])
+    axis /= np.linalg.norm(axis)
+    R0 = oracle.se3_exp(np.r_[axis * np.deg2rad(7.0), 0.0, 0.0, 0.0])
+    T_init = np.stack([R0 @ Tgt[p] for p in range(n)])
+    ds = torch.from_numpy(np.ascontiguousarray(src)).cuda()
+    dd = torch.from_numpy(np.ascontiguousarray(dst)).cuda()
+    torch.cuda.synchronize()
+    with youth_icp.IcpContext(W, H, max(n, 2), iters=1, dist_thresh=1.0) as ctx:
+        ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), n, T_init=T_init)
+        ctx.sync()
+        T64, _, st = ctx.get_poses(n)
+    for p in sorted({0, n - 1}):
+        T64o, _, sto, _ = oracle.align(src[p], dst[p], iters=1, dist_thresh=1.0,
+                                       T_init=T_init[p])
+        assert st[p] == sto == 0
+        step = np.arccos(np.clip((np.trace(T64o[:3, :3] @ T_init[p][:3, :3].T) - 1) / 2, -1, 1))
+        assert step > np.deg2rad(5.1), np.rad2deg(step)
+        assert _pose_err(T64[p], T64o) <= POSE_TOL, p
+    neq = oracle.reduce(src[0], dst[0], T_init[0][:3].astype(np.float32), oracle.viewer_K(W, H),
+                        dist_thresh=1.0)
+    xi, st0 = oracle.solve(neq)
+    assert st0 == 0 and np.linalg.norm(xi[:3]) ** 2 >= 2.0 ** -7
+    with youth_icp.IcpContext(W, H, 2) as ctx:
+        Tg, stg = ctx.solve(neq, T_init[0])
+    assert stg == 0 and np.abs(Tg - oracle.se3_exp(xi) @ T_init[0]).max() < 1e-12
+
+
 def test_context_device_api_poses_and_stats():
     n = 6
     src, dst, _ = youth_synth.pairs(20, n)
