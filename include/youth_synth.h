@@ -34,6 +34,9 @@ extern "C" {
 /* Flags for the generators. */
 #define YOUTH_SYNTH_NOISE 1 /* add depth-dependent Gaussian noise (sigma = 0.25 mm * Z^2) */
 #define YOUTH_SYNTH_HOLES 2 /* ~2 % random invalid pixels */
+/* SURVEY §8d's optional noise level, sigma = 1.5 mm * Z^2 (replaces
+ * YOUTH_SYNTH_NOISE's 0.25 when set): parity tests / bench leg only */
+#define YOUTH_SYNTH_NOISE_SURVEY 4
 
 /* Render one frame from the camera pose T_wc (4x4 row-major fp64; camera
  * frame x right, y down, z forward; world z up). */

@@ -1947,6 +1947,7 @@ struct youth_icp_ctx {
     int coop_px = 0;                 // YOUTH_ICP_COOP_PX: force pixels per lane (0: plan)
     int coop_threads = 512;          // YOUTH_ICP_COOP_THREADS=256: one wave per SIMD
     int coop_max_pairs = kCoopMaxPairs;  // YOUTH_ICP_COOP_MAX_PAIRS (<= kCoopMaxPairs)
+    int coop_launch = 0;             // YOUTH_ICP_COOP_LAUNCH: 0 serial (default), 1 runtime, 2 plain
     int coop_bpc[2][kCoopMaxPx + 1] = {};  // occupancy of k_icp_coop<fast> at npx (LDS)
     unsigned* d_coop = nullptr;      // 2 counter sets of kCoopSetWords
     int coop_par = 0;                // set used by the next coop call
@@ -2196,6 +2197,66 @@ struct PrepJob {
     bool wait;
 };
 
+// k_icp_coop's workgroups poll each other, so all n_pairs x G of them must be
+// resident together.  The planner sizes the grid to the co-resident capacity
+// of an idle device; what remains is another spin-waiting grid occupying the
+// CUs at the same time.  In this library that can only be another
+// k_icp_coop (k_icp never waits on a workgroup that is not running), so the
+// cooperative launches of a device are totally ordered instead, and launched
+// as plain kernels: hipLaunchCooperativeKernel's runtime path costs ~20 us
+// per launch on ROCm 7 (single-pair aligns/s 9.2 K against 11.3 K,
+// profiles/r02/stream_probe.txt).
+//   * While every coop launch of the device has come from ONE stream, stream
+//     order is the total order: no extra packet.
+//   * The first launch from a second stream switches the device to ordered
+//     mode for good: it waits for an event recorded on the previous stream at
+//     that moment (everything enqueued there so far, the last coop grid
+//     included), and from then on every coop launch records the device's
+//     completion event and waits on it when its stream differs from the
+//     previous launch's (an event record costs ~2.7 us per launch: 10.9 K).
+// YOUTH_ICP_COOP_LAUNCH=runtime restores hipLaunchCooperativeKernel.
+struct CoopOrder {
+    std::mutex mu;
+    hipStream_t last = nullptr;
+    hipEvent_t done = nullptr;
+    bool any = false;
+    bool multi = false;  // launches seen from more than one stream
+};
+static CoopOrder g_coop_order[64];
+
+static int coop_enqueue(youth_icp_ctx* c, hipStream_t s, void** args, int blocks, int npx)
+{
+    const void* kern = coop_kernel(c->fast, c->coop_threads);
+    const dim3 grid((unsigned)blocks), block(c->coop_threads);
+    const unsigned lds = (unsigned)coop_lds(npx, c->coop_threads);
+    if (c->coop_launch == 1) {
+        HIP_TRY(hipLaunchCooperativeKernel(kern, grid, block, args, lds, s));
+        return YOUTH_OK;
+    }
+    if (c->coop_launch == 2 || c->device < 0 || c->device >= 64) {  // unordered (probe only)
+        HIP_TRY(hipLaunchKernel(kern, grid, block, args, lds, s));
+        return YOUTH_OK;
+    }
+    CoopOrder& o = g_coop_order[c->device];
+    std::lock_guard<std::mutex> lk(o.mu);
+    if (o.any && o.last != s) {
+        if (!o.done) HIP_TRY(hipEventCreateWithFlags(&o.done, hipEventDisableTiming));
+        if (!o.multi) {
+            // first switch: mark the previous stream's work now (a stream the
+            // caller has destroyed since is rejected by the runtime: its work
+            // was released with it)
+            if (hipEventRecord(o.done, o.last) != hipSuccess) (void)hipGetLastError();
+            o.multi = true;
+        }
+        HIP_TRY(hipStreamWaitEvent(s, o.done, 0));
+    }
+    HIP_TRY(hipLaunchKernel(kern, grid, block, args, lds, s));
+    if (o.multi) HIP_TRY(hipEventRecord(o.done, s));
+    o.last = s;
+    o.any = true;
+    return YOUTH_OK;
+}
+
 static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, PairMap pm,
                        int n_pairs, const double* dTi, float* d_T_out, int npx, int G,
                        const PrepJob* job)
@@ -2223,9 +2284,8 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
     EventPair ep{};
     rc = ev_begin(c, s, &ep, 0);
     if (rc) return rc;
-    HIP_TRY(hipLaunchCooperativeKernel(coop_kernel(c->fast, c->coop_threads),
-                                       dim3((unsigned)(n_pairs * G)), dim3(c->coop_threads), args,
-                                       (unsigned)coop_lds(npx, c->coop_threads), s));
+    rc = coop_enqueue(c, s, args, n_pairs * G, npx);
+    if (rc) return rc;
     c->last_coop_G = G;
     c->last_coop_px = npx;
     return ev_end(c, s, &ep);
@@ -2516,6 +2576,8 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         c->coop = !(nc && *nc && *nc != '0');
         const char* cpx = getenv("YOUTH_ICP_COOP_PX");
         if (cpx && atoi(cpx) >= 1 && atoi(cpx) <= kCoopMaxPx) c->coop_px = atoi(cpx);
+        const char* cl = getenv("YOUTH_ICP_COOP_LAUNCH");
+        c->coop_launch = !cl ? 0 : strcmp(cl, "runtime") == 0 ? 1 : strcmp(cl, "plain") == 0 ? 2 : 0;
         const char* cmp = getenv("YOUTH_ICP_COOP_MAX_PAIRS");
         if (cmp && atoi(cmp) >= 0) c->coop_max_pairs = atoi(cmp);
     }

@@ -143,9 +143,10 @@ void youth_synth_render(const double T_wc[16], int W, int H,
             const double g1 = (double)((splitmix64(&rng) >> 11) + 1) * 0x1.0p-53;
             const double g2 = u01(&rng);
             double zmm = z * (double)K->depth_scale;
-            if (flags & YOUTH_SYNTH_NOISE) {
+            if (flags & (YOUTH_SYNTH_NOISE | YOUTH_SYNTH_NOISE_SURVEY)) {
                 const double g = sqrt(-2.0 * log(g1)) * cos(2.0 * M_PI * g2);
-                zmm += g * 0.25 * z * z * ((double)K->depth_scale / 1000.0);
+                const double sigma = (flags & YOUTH_SYNTH_NOISE_SURVEY) ? 1.5 : 0.25;
+                zmm += g * sigma * z * z * ((double)K->depth_scale / 1000.0);
             }
             double dq = floor(zmm + 0.5);
             const double lo = 0.4 * (double)K->depth_scale, hi = 8.0 * (double)K->depth_scale;

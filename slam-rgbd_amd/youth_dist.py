@@ -22,6 +22,15 @@ def pair_shard(rank: int, pairs_per_rank: int) -> tuple[int, int]:
     return rank * pairs_per_rank, pairs_per_rank
 
 
+def pair_range(n_pairs: int, world: int, rank: int) -> tuple[int, int]:
+    """(first global pair index, count) of `rank` when ONE batch of n_pairs is
+    split into contiguous shards (strong scaling, SURVEY §8e: 512 pairs ->
+    512/256/128/64 per GPU at N = 1/2/4/8); the first n_pairs % world ranks
+    take one extra pair."""
+    base, extra = divmod(n_pairs, world)
+    return rank * base + min(rank, extra), base + (1 if rank < extra else 0)
+
+
 def sequence_shard(n_frames: int, world: int, rank: int) -> tuple[int, int]:
     """Frames [f0, f1) held by `rank` so that its pairs (k, k+1), k in
     [f0, f1-1), tile the F-1 pairs exactly once across ranks; the last frame
@@ -37,8 +46,10 @@ def sequence_shard(n_frames: int, world: int, rank: int) -> tuple[int, int]:
 
 
 def gather_poses(local: torch.Tensor, world: int) -> torch.Tensor:
-    """All-gather [n, 16] pose rows from every rank, rank-ordered."""
-    if world == 1:
+    """All-gather [n, 16] pose rows from every rank, rank-ordered.  World 1
+    returns `local` unless a process group is up (then the collective runs:
+    the one-GPU RCCL check of bench.py, YOUTH_BENCH_DIST=1)."""
+    if world == 1 and not dist.is_initialized():
         return local
     out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
                       device=local.device)
@@ -60,11 +71,25 @@ def gather_poses_async(local: torch.Tensor, out: torch.Tensor, world: int):
     tensors, synchronous).
     Callers double-buffer `local` / `out` so the next align overlaps the
     gather of the previous one."""
-    if world == 1:
+    if world == 1 and not dist.is_initialized():
         return None   # nothing to gather: `out` is not written
     if dist.get_backend() == "nccl":
         return dist.all_gather_into_tensor(out, local.contiguous(), async_op=True)
     out.copy_(gather_poses(local, world))
+    return None
+
+
+def gather_poses_ragged_async(local: torch.Tensor, out: torch.Tensor, world: int,
+                              counts: list[int]):
+    """gather_poses_async for shards of rank-dependent size (counts[r] rows on
+    rank r, pair_range): equal shards take the single RCCL all-gather, ragged
+    ones are padded to the largest shard (synchronous).  Returns the work
+    handle or None (world 1: nothing to gather, `out` untouched)."""
+    if world == 1 and not dist.is_initialized():
+        return None
+    if all(c == counts[0] for c in counts):
+        return gather_poses_async(local, out, world)
+    out.copy_(gather_ragged(local, world, max(counts), counts))
     return None
 
 
@@ -73,7 +98,7 @@ def gather_ragged(local: torch.Tensor, world: int, max_rows: int,
     """All-gather [m_r, 16] rows with different m_r per rank (sequence
     shards): pad to max_rows, gather the rows (and the counts, unless the
     caller knows them: sequence_shard gives every rank's), strip padding."""
-    if world == 1:
+    if world == 1 and not dist.is_initialized():
         return local
     pad = torch.zeros((max_rows,) + tuple(local.shape[1:]), dtype=local.dtype,
                       device=local.device)

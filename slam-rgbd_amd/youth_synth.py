@@ -18,6 +18,8 @@ PAIR_SEED = 0x5EED0000
 SEQ_SEED = 0x5EED1000
 NOISE = 1
 HOLES = 2
+NOISE_SURVEY = 4   # SURVEY §8d sigma = 1.5 mm * Z^2 (instead of NOISE's 0.25)
+SURVEY_FLAGS = NOISE_SURVEY | HOLES
 DEFAULT_FLAGS = NOISE | HOLES
 
 _lib = None

@@ -30,31 +30,42 @@ def _port():
 
 
 def test_bench_single_gpu_contract():
-    r = subprocess.run([sys.executable, "bench.py", "--steps", "3", "--warmup", "1"], cwd=ROOT,
-                       capture_output=True, text=True, timeout=600)
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "3", "--warmup", "1",
+                        "--global-pairs", "64", "--windows", "1", "--c3-pairs", "2",
+                        "--c5-frames", "41"], cwd=ROOT, capture_output=True, text=True,
+                       timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     d = _json_line(r.stdout)
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
               "roofline", "cpu_baseline"):
         assert k in d, k
-    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["value"] > 0 and d["scaling"] == "weak"
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["value"] > 0 and d["scaling"] == "strong"
     assert d["higher_is_better"] is True and d["unit"] == "aligns/s"
-    assert d["config"]["workload"].startswith("C4") and d["config"]["pairs_per_gpu"] == 64
+    assert d["config"]["workload"].startswith("C4") and d["config"]["global_pairs"] == 64
+    assert len(d["window_rates"]) == 1 and d["status_nonzero"] == 0
     rf = d["roofline"]
-    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "survey_model"):
         assert k in rf, k
-    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and 0 < rf["frac"] < 1.2
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and 0 < rf["frac"] < 1.0
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9
+    assert rf["iterations_per_launch"] == 10
+    rp = d["roofline_prep"]
+    assert rp["kernel"] == "k_prep" and 0 < rp["frac"] < 1.0
     cb = d["cpu_baseline"]
-    for k in ("value", "unit", "cores", "kind", "sample"):
+    for k in ("value", "unit", "cores", "kind", "sample", "threads_share", "threads_all"):
         assert k in cb, k
     assert cb["kind"] == "port" and cb["value"] > 0
     assert d["parity"]["pose_max_abs_err_vs_cpu"] <= 1e-5
-    sp = d["single_pair"]                   # C2 leg: one pair per call, small-batch kernel
-    assert sp["value"] > 0 and sp["status"] == 0 and sp["pose_max_abs_err_vs_cpu"] <= 1e-5
-    assert sp["kernel_path"]["kernel"] == "k_icp_coop"
+    assert d["parity"]["survey_noise"]["pose_max_abs_err_vs_cpu"] <= 1e-5
+    c2 = d["c2"]                            # one pair per call, small-batch kernel
+    assert c2["value"] > 0 and c2["status"] == 0 and c2["pose_max_abs_err_vs_cpu"] <= 1e-5
+    assert c2["kernel_path"]["kernel"] == "k_icp_coop"
+    assert d["c3"]["parity_ok"] and d["c3"]["batch"]["pairs_per_call"] == 2
+    assert d["c5"]["parity_ok"] and d["c5"]["batch"]["trajectory_frames"] == 41
+    assert d["c5"]["streamed"]["max_abs_diff_vs_batch_poses"] <= 1e-5
     assert d["kernel_path"]["kernel"].startswith("k_prep + k_icp")
+    assert d["viewer_cloud"]["bit_exact_vs_cpu"]
 
 
 @pytest.mark.parametrize("workload", ["pairs", "sequence"])
@@ -62,7 +73,8 @@ def test_bench_two_ranks_rehearsal(workload):
     env = dict(os.environ, YOUTH_BENCH_BACKEND="gloo")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus",
-           "2", "--steps", "3", "--warmup", "1", "--workload", workload]
+           "2", "--steps", "3", "--warmup", "1", "--windows", "1", "--workload", workload,
+           "--global-pairs", "128"]
     if workload == "sequence":
         cmd += ["--frames", "41"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
@@ -70,7 +82,28 @@ def test_bench_two_ranks_rehearsal(workload):
     d = _json_line(r.stdout)
     assert d["n_gpus"] == 2 and d["value"] > 0
     if workload == "pairs":
-        assert d["scaling"] == "weak" and d["config"]["global_pairs"] == 128
+        assert d["scaling"] == "strong" and d["config"]["global_pairs"] == 128
+        assert d["config"]["pairs_per_gpu"] == 64
     else:
         assert d["scaling"] == "strong" and d["config"]["pairs"] == 40
     assert "cpu_baseline" not in d          # rank 0 at N=1 only
+
+
+@pytest.mark.parametrize("workload", ["pairs", "sequence"])
+def test_bench_rccl_gather_one_gpu(workload):
+    """The RCCL path itself on hardware: one rank with the process group up
+    (YOUTH_BENCH_DIST=1, backend nccl = RCCL): init_process_group(device_id=),
+    all_gather_into_tensor(async_op=True) + handle.wait() on the side stream,
+    the ragged sequence gather, max-over-ranks timing.  bench.py raises if the
+    gathered / host rows differ from the rank's poses."""
+    env = dict(os.environ, YOUTH_BENCH_DIST="1")
+    env.pop("YOUTH_BENCH_BACKEND", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus",
+           "1", "--steps", "3", "--warmup", "1", "--windows", "1", "--workload", workload,
+           "--global-pairs", "32", "--frames", "21", "--no-legs", "--no-cpu-baseline",
+           "--no-host-io", "--no-viewer"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 1 and d["value"] > 0

@@ -22,6 +22,7 @@ usage: tools/pmc_traffic.py <profile_root> <out.json> <pairs> <width> <height> [
 """
 import csv
 import glob
+import hashlib
 import json
 import os
 import sys
@@ -50,6 +51,11 @@ def main():
         "hbm_bytes_per_iteration": (2.0 * fetch + write) / iters,
         "bytes_per_px": (2.0 * fetch + write) / iters / px,
         "correction": "2 x FETCH_SIZE (gfx950 tallies 128-B requests as 64 B)",
+        # bench.py uses these figures only for the kernel source they were taken on
+        "kernel_sha16": hashlib.sha256(open(os.path.join(
+            os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "slam-rgbd_amd", "csrc",
+            "icp_kernels.hip"), "rb").read()).hexdigest()[:16],
+        "profile_root": root,
     }
     if "SQ_INSTS_VALU" in r and "GRBM_GUI_ACTIVE" in r:
         simds = 1024
@@ -63,6 +69,13 @@ def main():
         doc["valu_cycles_per_instruction"] = simds * cyc / r["SQ_INSTS_VALU"]
         doc["gpu_cycles_per_launch"] = cyc
         doc["simds"] = simds
+        if "SQ_ACTIVE_INST_VALU" in r:
+            # rocprof's derived VALUBusy: 4 x SQ_ACTIVE_INST_VALU (quad-cycles) /
+            # SIMDs / GRBM_GUI_ACTIVE (per XCD); ~1 = a VALU instruction in
+            # execution on every SIMD in every cycle of the kernel
+            doc["valu_busy_frac"] = 4.0 * r["SQ_ACTIVE_INST_VALU"] / simds / cyc
+            doc["valu_busy_definition"] = ("4 x SQ_ACTIVE_INST_VALU / SIMDs / (GRBM_GUI_ACTIVE / "
+                                           "8 XCDs) (rocprof VALUBusy)")
         durs = []
         for f in glob.glob(os.path.join(root, "*", "*kernel_trace.csv")):
             if "sq" not in os.path.basename(os.path.dirname(f)):

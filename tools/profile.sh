@@ -6,7 +6,7 @@
 # Usage: tools/profile.sh <tag> [bench args...]
 set -euo pipefail
 TAG=${1:-r01}; shift || true
-ARGS=${*:---steps 30 --warmup 5 --no-cpu-baseline --no-host-io --no-single-pair}
+ARGS=${*:---steps 30 --warmup 5 --windows 0 --no-cpu-baseline --no-host-io --no-legs --no-viewer}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
