@@ -206,11 +206,12 @@ int youth_icp_get_sched_stats(youth_icp_ctx* ctx, unsigned* spins,
  * negative on error.  Either pointer may be NULL. */
 int youth_icp_get_plan(youth_icp_ctx* ctx, int* workgroups_per_pair, int* px_per_lane);
 
-/* Validation: compare the kernels' shared-reciprocal projection division with
- * IEEE fp32 a/b on n pseudo-random cases (seeded) on `device`.
- * *bit_mismatches counts bitwise differences where the IEEE expansion does not
- * rescale (must be 0); *proj_mismatches counts differences of the projected
- * pixel floor((q + c) + 0.5) or its in-range test over all cases (must be 0). */
+/* Validation of the projection reciprocal rz = RN(1 / z') the kernels form
+ * from v_rcp_f32 plus correction steps: *bit_mismatches counts bitwise
+ * differences from IEEE 1.0f / den over EVERY fp32 den in the guarded range
+ * [2^-60, 2^60] (must be 0); *proj_mismatches counts differences of the
+ * projected pixel floor(fma(num, rz, c) + 0.5) or its in-range test against
+ * the IEEE reciprocal's on n pseudo-random (seeded) cases (must be 0). */
 int youth_icp_selftest_projdiv(int device, long long n, unsigned long long seed,
                                long long* bit_mismatches, long long* proj_mismatches);
 

@@ -86,19 +86,22 @@ static inline int assoc_one(float sx, float sy, float sz, const float T[12],
                             float thr2, float q[3])
 {
     if (!(sz > 0.0f)) return -1;
-    const float qx = ((T[0] * sx + T[1] * sy) + T[2] * sz) + T[3];
-    const float qy = ((T[4] * sx + T[5] * sy) + T[6] * sz) + T[7];
-    const float qz = ((T[8] * sx + T[9] * sy) + T[10] * sz) + T[11];
+    /* P' = R P + t as three fma chains (one rounding per step) */
+    const float qx = fmaf(T[2], sz, fmaf(T[1], sy, fmaf(T[0], sx, T[3])));
+    const float qy = fmaf(T[6], sz, fmaf(T[5], sy, fmaf(T[4], sx, T[7])));
+    const float qz = fmaf(T[10], sz, fmaf(T[9], sy, fmaf(T[8], sx, T[11])));
     if (!(qz > 0.0f)) return -1;
-    const float fu = floorf((((K->fx * qx) / qz) + K->cx) + 0.5f);
-    const float fv = floorf((((K->fy * qy) / qz) + K->cy) + 0.5f);
+    /* one correctly rounded reciprocal, then fx P'x rz + cx in one rounding */
+    const float rz = 1.0f / qz;
+    const float fu = floorf(fmaf(K->fx * qx, rz, K->cx) + 0.5f);
+    const float fv = floorf(fmaf(K->fy * qy, rz, K->cy) + 0.5f);
     if (!(fu >= 0.0f && fu < (float)W && fv >= 0.0f && fv < (float)H)) return -1;
     const int j = (int)fv * W + (int)fu;
     const float tz = tZ[j];
     if (!(tz > 0.0f)) return -1;
     if (nX[j] == 0.0f && nY[j] == 0.0f && nZ[j] == 0.0f) return -1;
     const float dx = qx - tX[j], dy = qy - tY[j], dz = qz - tz;
-    const float d2 = (dx * dx + dy * dy) + dz * dz;
+    const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
     if (!(d2 < thr2)) return -1;
     q[0] = qx;
     q[1] = qy;
@@ -138,12 +141,12 @@ void oracle_reduce(const float* sX, const float* sY, const float* sZ,
         const float nx = nX[j], ny = nY[j], nz = nZ[j];
         const float dx = q[0] - tX[j], dy = q[1] - tY[j], dz = q[2] - tZ[j];
         /* residual r = n . (P' - P_t)  (spec a8) */
-        const float r = (nx * dx + ny * dy) + nz * dz;
+        const float r = fmaf(nz, dz, fmaf(ny, dy, nx * dx));
         /* J = [ (P' x n)^T , n^T ]  for the left perturbation exp(xi) T */
         float J[6];
-        J[0] = q[1] * nz - q[2] * ny;
-        J[1] = q[2] * nx - q[0] * nz;
-        J[2] = q[0] * ny - q[1] * nx;
+        J[0] = fmaf(q[1], nz, -(q[2] * ny));
+        J[1] = fmaf(q[2], nx, -(q[0] * nz));
+        J[2] = fmaf(q[0], ny, -(q[1] * nx));
         J[3] = nx;
         J[4] = ny;
         J[5] = nz;

@@ -141,6 +141,19 @@ __device__ __forceinline__ bool proj_den_ok(float den)
 {
     return (den >= 0x1p-60f) & (den <= 0x1p60f);
 }
+// Spec a7's projection reciprocal RN(1 / den): for den in [2^-60, 2^60] the
+// IEEE expansion of 1.0f / den rescales nothing (numerator 1, quotient in
+// [2^-60, 2^60]), so the chain reduces to the reciprocal refined by the two
+// correction steps of proj_div_one; youth_icp_selftest_projdiv compares it
+// with 1.0f / den for EVERY fp32 den in that range.  Outside: IEEE.
+__device__ __forceinline__ float proj_rcp_rn(float den)
+{
+    if (proj_den_ok(den)) {  // always in practice (den is a depth in metres)
+        const float r = proj_recip(den);
+        return proj_div_one(1.0f, den, r);
+    }
+    return 1.0f / den;
+}
 
 // Spec a6's normalisation n = c / sqrtf(|c|^2) on its common range, bit for
 // bit.  hipcc's correctly rounded sqrtf is  x' = x < 2^-96 ? x 2^32 : x;
@@ -209,17 +222,14 @@ __global__ void k_verify_fastdiv(Intr K, FastK F, int W, int H, unsigned* bad)
     if (nb) atomicAdd(bad, nb);
 }
 
-// Bitwise self-test of the shared-reciprocal projection division
-// (proj_recip / proj_div_one) against IEEE a/b on `n` SplitMix64 cases:
-//   mode 0: random den in [2^-60, 2^60], num with exponent in [-80, 80];
-//   mode 1: quotients next to half-integers (the rounding-critical case of
-//           floor(q + c + 0.5)): num = RN(den * (m + 0.5)) +- a few ulps;
-//   mode 2: den in range, num any finite fp32 bit pattern (incl. 0, tiny,
-//           denormal, huge);
-//   mode 3: den near the guard bounds 2^+-60, num random.
-// bad[0]: bit mismatches where div_scale does not rescale (must be 0);
-// bad[1]: mismatches of the projection outcome floor((q + c) + 0.5) and its
-//         in-range test [0, 65536) for c in [0, 4096) (must be 0), all cases.
+// Self-test of the projection reciprocal (proj_rcp_rn) against IEEE 1.0f / den:
+// bad[0]: bitwise mismatches over EVERY fp32 den in [2^-60, 2^60] (the
+//         guarded range: exhaustive, ~1.0e9 values; must be 0);
+// bad[1]: mismatches of the projected pixel floor(fma(num, rz, c) + 0.5) and
+//         its in-range test [0, 65536) between proj_rcp_rn and 1.0f / den on
+//         `n` SplitMix64 cases (den any positive finite fp32 incl. outside the
+//         guard, num random with exponent in [-80, 80] or next to a
+//         half-integer quotient, c in [0, 4096); must be 0).
 __device__ __forceinline__ unsigned long long sm64(unsigned long long& x)
 {
     unsigned long long z = (x += 0x9E3779B97F4A7C15ull);
@@ -232,45 +242,30 @@ __global__ void k_selftest_projdiv(unsigned long long n, unsigned long long seed
 {
     unsigned long long b0 = 0, b1 = 0;
     const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += stride) {
+    const unsigned long long tid = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    constexpr unsigned kLo = 0x21800000u, kHi = 0x5D800000u;  // 2^-60, 2^60
+    for (unsigned long long b = kLo + tid; b <= kHi; b += stride) {
+        const float den = __uint_as_float((unsigned)b);
+        b0 += __float_as_uint(proj_rcp_rn(den)) != __float_as_uint(1.0f / den);
+    }
+    for (unsigned long long i = tid; i < n; i += stride) {
         unsigned long long st = seed ^ (i * 0xD1B54A32D192ED03ull);
         const unsigned long long r1 = sm64(st), r2 = sm64(st), r3 = sm64(st);
-        const int mode = (int)(i & 3);
-        float den;
-        if (mode == 3) {
-            const int e = (r1 & 1) ? 60 : -60;
-            den = __uint_as_float((unsigned)((e + 127) << 23) | (unsigned)(r2 & 0x7FFFFF));
-            if (r1 & 2) den = __uint_as_float(__float_as_uint(den) - (unsigned)((r3 >> 40) & 0xFF));
-        } else {
-            const int e = (int)(r1 % 121) - 60;
-            den = __uint_as_float((unsigned)((e + 127) << 23) | (unsigned)(r2 & 0x7FFFFF));
-        }
+        const int ed = (i & 7) == 7 ? (int)(r1 % 254) - 126 : (int)(r1 % 121) - 60;
+        const float den = __uint_as_float((unsigned)((ed + 127) << 23) | (unsigned)(r2 & 0x7FFFFF));
         float num;
-        if (mode == 1) {
+        if (i & 1) {  // quotient next to a half-integer: the rounding-critical case
             const float m = (float)((int)(r3 % 8192) - 4096) + 0.5f;
             num = den * m;
             num = __uint_as_float(__float_as_uint(num) + (unsigned)((int)((r3 >> 20) & 7) - 3));
-        } else if (mode == 2) {
-            unsigned bits = (unsigned)(r3 >> 8);
-            if (((bits >> 23) & 0xFF) == 0xFF) bits &= ~(1u << 30);  // finite only
-            num = __uint_as_float(bits);
         } else {
             const int e = (int)((r3 >> 8) % 161) - 80;
             num = __uint_as_float((unsigned)((e + 127) << 23) | (unsigned)(r3 & 0x7FFFFF) |
                                   (unsigned)((r3 >> 63) << 31));
         }
-        if (!proj_den_ok(den)) continue;
-        const float q_ieee = num / den;
-        const float q_fast = proj_div_one(num, den, proj_recip(den));
-        const float aq = fabsf(q_ieee), an = fabsf(num);
-        const int en = (int)((__float_as_uint(num) >> 23) & 0xFF);
-        const int ed = (int)((__float_as_uint(den) >> 23) & 0xFF);
-        const bool noscale = num != 0.0f && en - ed < 96 && en > 23 && aq >= 0x1p-126f &&
-                             an == an;
-        if (noscale && __float_as_uint(q_ieee) != __float_as_uint(q_fast)) ++b0;
         const float c = (float)(r2 >> 52);  // [0, 4096)
-        const float ui = floorf((q_ieee + c) + 0.5f), uf = floorf((q_fast + c) + 0.5f);
+        const float ui = floorf(fmaf(num, 1.0f / den, c) + 0.5f);
+        const float uf = floorf(fmaf(num, proj_rcp_rn(den), c) + 0.5f);
         const bool ii = (ui >= 0.0f) & (ui < 65536.0f), inf_ = (uf >= 0.0f) & (uf < 65536.0f);
         if (ii != inf_ || (ii && ui != uf)) ++b1;
     }
@@ -891,6 +886,77 @@ struct PoseState {
     int it, iters;
 };
 
+// ------------------------------------------------- spec a7-a9 per pixel --
+// Shared by k_reduce / k_icp (accumulate_chunk) and k_icp_coop (coop_group);
+// oracle/icp_oracle.c assoc_one / oracle_reduce evaluate the same operations
+// with the same roundings (fmaf = one rounding, -ffp-contract=off elsewhere).
+//   a7  P' = R P + t:  P'_i = fma(R_i2, z, fma(R_i1, y, fma(R_i0, x, t_i)))
+//       valid iff z > 0 and P'_z > 0;  rz = RN(1 / P'_z);
+//       u' = floor(fma(fx P'_x, rz, cx) + 0.5), v' likewise; in range of the
+//       target frame.  Unmatched pixels compute on safe values (branch-free)
+//       and gather record 0.
+__device__ __forceinline__ void xform_project(const float* T, float sx, float sy, float sz,
+                                              const Intr& K, int W, int H, float& qx, float& qy,
+                                              float& qz, float& fu, float& fv, bool& in, int& j)
+{
+    qx = fmaf(T[2], sz, fmaf(T[1], sy, fmaf(T[0], sx, T[3])));
+    qy = fmaf(T[6], sz, fmaf(T[5], sy, fmaf(T[4], sx, T[7])));
+    qz = fmaf(T[10], sz, fmaf(T[9], sy, fmaf(T[8], sx, T[11])));
+    const bool vz = (sz > 0.0f) & (qz > 0.0f);
+    const float rz = proj_rcp_rn(vz ? qz : 1.0f);
+    const float uu = floorf(fmaf(K.fx * qx, rz, K.cx) + 0.5f);
+    const float vv = floorf(fmaf(K.fy * qy, rz, K.cy) + 0.5f);
+    in = vz & (uu >= 0.0f) & (uu < (float)W) & (vv >= 0.0f) & (vv < (float)H);
+    fu = in ? uu : 0.0f;
+    fv = in ? vv : 0.0f;
+    // 0 when !in; v', W <= 16384 (youth_icp_create): the 24-bit multiply is
+    // exact and full rate
+    j = (int)__umul24((unsigned)(int)fv, (unsigned)W) + (int)fu;
+}
+
+//   a7  gate: target valid with a normal (k_prep stores z = 0 for a target
+//       without one, so tz > 0 is both tests) and |P' - P_t|^2 < thr^2 with
+//       d2 = fma(dz, dz, fma(dy, dy, dx dx));
+//   a8  r = n.(P' - P_t) = fma(n2, dz, fma(n1, dy, n0 dx));
+//       J = [P' x n, n], (P' x n)_0 = fma(qy, n2, -(qz n1)) etc.;
+//   a9  the 28 products of fp32 values are exact in fp64; one rounding per
+//       add.  Unmatched: the normal is masked to 0, so J = 0 and r = +-0 leave
+//       every sum unchanged.  The target's x, y are recomputed from its z with
+//       k_prep's expression (bit-identical to the stored plane).
+template <bool kFast>
+__device__ __forceinline__ bool match_accumulate(float qx, float qy, float qz, f4v t, float fu,
+                                                 float fv, bool in, const Intr& K,
+                                                 const FastK& F, float thr2, double* acc)
+{
+    const float tz = t.x;
+    const float tx = bp_div<kFast>((fu - K.cx) * tz, K.fx, F.rfx);
+    const float ty = bp_div<kFast>((fv - K.cy) * tz, K.fy, F.rfy);
+    const float dx = qx - tx, dy = qy - ty, dz = qz - tz;
+    const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+    const bool ok = in & (tz > 0.0f) & (d2 < thr2);
+    const float n0 = ok ? t.y : 0.0f, n1 = ok ? t.z : 0.0f, n2 = ok ? t.w : 0.0f;
+    const float r = fmaf(n2, dz, fmaf(n1, dy, n0 * dx));
+    float Jf[6];
+    Jf[0] = fmaf(qy, n2, -(qz * n1));
+    Jf[1] = fmaf(qz, n0, -(qx * n2));
+    Jf[2] = fmaf(qx, n1, -(qy * n0));
+    Jf[3] = n0;
+    Jf[4] = n1;
+    Jf[5] = n2;
+    int k = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int bb = a; bb < 6; ++bb) {
+            acc[k] = fma((double)Jf[a], (double)Jf[bb], acc[k]);
+            ++k;
+        }
+#pragma unroll
+    for (int a = 0; a < 6; ++a) acc[21 + a] = fma((double)Jf[a], (double)r, acc[21 + a]);
+    acc[27] = fma((double)r, (double)r, acc[27]);
+    return ok;
+}
+
 // Accumulate source pixels [start, end) of one pair into acc (spec a7-a9).
 template <bool kAssoc, bool kFast, bool kAligned>
 __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
@@ -919,7 +985,6 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
     for (; i < end; i += kRedStep) {
         const short4 d4 = load_depth4<kAligned>(sD, i, end);
         const int dd[4] = {d4.x, d4.y, d4.z, d4.w};
-        // spec a7: P' = R P + t (fixed order, no FMA); projective association
         float qx[4], qy[4], qz[4], fu[4], fv[4];
         bool in[4];
         int j[4];
@@ -933,29 +998,7 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
             }
             float sx, sy, sz;
             backproject<kFast>(kAligned || (i + q) < end ? dd[q] : 0, u, v, K, F, sx, sy, sz);
-            qx[q] = ((T[0] * sx + T[1] * sy) + T[2] * sz) + T[3];
-            qy[q] = ((T[4] * sx + T[5] * sy) + T[6] * sz) + T[7];
-            qz[q] = ((T[8] * sx + T[9] * sy) + T[10] * sz) + T[11];
-            const bool vz = (sz > 0.0f) & (qz[q] > 0.0f);
-            const float qzs = vz ? qz[q] : 1.0f;
-            const float nu = K.fx * qx[q], nv = K.fy * qy[q];
-            float du, dv;
-            if (proj_den_ok(qzs)) {  // always in practice (qz is a depth in metres)
-                const float r = proj_recip(qzs);
-                du = proj_div_one(nu, qzs, r);
-                dv = proj_div_one(nv, qzs, r);
-            } else {
-                du = nu / qzs;
-                dv = nv / qzs;
-            }
-            const float uu = floorf((du + K.cx) + 0.5f);
-            const float vv = floorf((dv + K.cy) + 0.5f);
-            in[q] = vz & (uu >= 0.0f) & (uu < (float)W) & (vv >= 0.0f) & (vv < (float)H);
-            fu[q] = in[q] ? uu : 0.0f;
-            fv[q] = in[q] ? vv : 0.0f;
-            // 0 when !in; v', W <= 16384 (youth_icp_create): the 24-bit
-            // multiply is exact and full rate
-            j[q] = (int)__umul24((unsigned)(int)fv[q], (unsigned)W) + (int)fu[q];
+            xform_project(T, sx, sy, sz, K, W, H, qx[q], qy[q], qz[q], fu[q], fv[q], in[q], j[q]);
         }
         u0 += stepU;
         v0 += stepV;
@@ -971,39 +1014,9 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
                                                                                  0, 0));
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const float tz = t[q].x;
-            const float tx = bp_div<kFast>((fu[q] - K.cx) * tz, K.fx, F.rfx);
-            const float ty = bp_div<kFast>((fv[q] - K.cy) * tz, K.fy, F.rfy);
-            const float nx = t[q].y, ny = t[q].z, nz = t[q].w;
-            const float dx = qx[q] - tx, dy = qy[q] - ty, dz = qz[q] - tz;
-            const float d2 = (dx * dx + dy * dy) + dz * dz;
-            // target valid AND normal valid: k_prep stores z = 0 for a target
-            // without a normal, so tz > 0 is both tests
-            const bool ok = in[q] & (tz > 0.0f) & (d2 < thr2);
+            const bool ok = match_accumulate<kFast>(qx[q], qy[q], qz[q], t[q], fu[q], fv[q], in[q],
+                                                    K, F, thr2, acc);
             if (kAssoc && (i + q) < end) arow[i + q] = ok ? j[q] : -1;
-            // spec a8: r = n.(P' - P_t); J = [P' x n, n]  (zeros when unmatched:
-            // with the masked normal r is +-0, which leaves every fp64 sum unchanged)
-            const float n0 = ok ? nx : 0.0f, n1 = ok ? ny : 0.0f, n2 = ok ? nz : 0.0f;
-            const float r = (n0 * dx + n1 * dy) + n2 * dz;
-            float Jf[6];
-            Jf[0] = qy[q] * n2 - qz[q] * n1;
-            Jf[1] = qz[q] * n0 - qx[q] * n2;
-            Jf[2] = qx[q] * n1 - qy[q] * n0;
-            Jf[3] = n0;
-            Jf[4] = n1;
-            Jf[5] = n2;
-            // spec a9: fp32 products are exact in fp64; one rounding per add
-            int k = 0;
-#pragma unroll
-            for (int a = 0; a < 6; ++a)
-#pragma unroll
-                for (int bb = a; bb < 6; ++bb) {
-                    acc[k] = fma((double)Jf[a], (double)Jf[bb], acc[k]);
-                    ++k;
-                }
-#pragma unroll
-            for (int a = 0; a < 6; ++a) acc[21 + a] = fma((double)Jf[a], (double)r, acc[21 + a]);
-            acc[27] = fma((double)r, (double)r, acc[27]);
             cnt += ok ? 1 : 0;
         }
     }
@@ -1574,27 +1587,7 @@ __device__ __forceinline__ void coop_group(const float* __restrict__ X, const fl
         const float sx = X[(s0 + q) * kThreads + t];
         const float sy = Y[(s0 + q) * kThreads + t];
         const float sz = Z[(s0 + q) * kThreads + t];
-        qx[q] = ((T[0] * sx + T[1] * sy) + T[2] * sz) + T[3];
-        qy[q] = ((T[4] * sx + T[5] * sy) + T[6] * sz) + T[7];
-        qz[q] = ((T[8] * sx + T[9] * sy) + T[10] * sz) + T[11];
-        const bool vz = (sz > 0.0f) & (qz[q] > 0.0f);
-        const float qzs = vz ? qz[q] : 1.0f;
-        const float nu = K.fx * qx[q], nv = K.fy * qy[q];
-        float du, dv;
-        if (proj_den_ok(qzs)) {
-            const float r = proj_recip(qzs);
-            du = proj_div_one(nu, qzs, r);
-            dv = proj_div_one(nv, qzs, r);
-        } else {
-            du = nu / qzs;
-            dv = nv / qzs;
-        }
-        const float uu = floorf((du + K.cx) + 0.5f);
-        const float vv = floorf((dv + K.cy) + 0.5f);
-        in[q] = vz & (uu >= 0.0f) & (uu < (float)W) & (vv >= 0.0f) & (vv < (float)H);
-        fu[q] = in[q] ? uu : 0.0f;
-        fv[q] = in[q] ? vv : 0.0f;
-        j[q] = (int)__umul24((unsigned)(int)fv[q], (unsigned)W) + (int)fu[q];
+        xform_project(T, sx, sy, sz, K, W, H, qx[q], qy[q], qz[q], fu[q], fv[q], in[q], j[q]);
     }
     f4v rec[Q];
 #pragma unroll
@@ -1602,32 +1595,8 @@ __device__ __forceinline__ void coop_group(const float* __restrict__ X, const fl
         rec[q] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rrec, j[q] * 16, 0, 0));
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-        const float tz = rec[q].x;
-        const float tx = bp_div<kFast>((fu[q] - K.cx) * tz, K.fx, F.rfx);
-        const float ty = bp_div<kFast>((fv[q] - K.cy) * tz, K.fy, F.rfy);
-        const float dx = qx[q] - tx, dy = qy[q] - ty, dz = qz[q] - tz;
-        const float d2 = (dx * dx + dy * dy) + dz * dz;
-        const bool ok = in[q] & (tz > 0.0f) & (d2 < thr2);
-        const float n0 = ok ? rec[q].y : 0.0f, n1 = ok ? rec[q].z : 0.0f, n2 = ok ? rec[q].w : 0.0f;
-        const float r = (n0 * dx + n1 * dy) + n2 * dz;
-        float Jf[6];
-        Jf[0] = qy[q] * n2 - qz[q] * n1;
-        Jf[1] = qz[q] * n0 - qx[q] * n2;
-        Jf[2] = qx[q] * n1 - qy[q] * n0;
-        Jf[3] = n0;
-        Jf[4] = n1;
-        Jf[5] = n2;
-        int kk = 0;
-#pragma unroll
-        for (int a = 0; a < 6; ++a)
-#pragma unroll
-            for (int bb = a; bb < 6; ++bb) {
-                acc[kk] = fma((double)Jf[a], (double)Jf[bb], acc[kk]);
-                ++kk;
-            }
-#pragma unroll
-        for (int a = 0; a < 6; ++a) acc[21 + a] = fma((double)Jf[a], (double)r, acc[21 + a]);
-        acc[27] = fma((double)r, (double)r, acc[27]);
+        const bool ok = match_accumulate<kFast>(qx[q], qy[q], qz[q], rec[q], fu[q], fv[q], in[q],
+                                                K, F, thr2, acc);
         nmatch += ok ? 1 : 0;
     }
 }

@@ -366,11 +366,12 @@ def test_algorithm_module_thread_entry(monkeypatch):
 
 
 # ------------------------------------------------ division path / alignment --
-def test_projection_division_matches_ieee():
-    """The shared-reciprocal projection divide (icp_kernels.hip proj_div_one)
-    equals IEEE a/b bit for bit wherever the IEEE expansion does not rescale,
-    and gives the same projected pixel / in-range decision everywhere:
-    2 x 2^30 random, near-half-integer, arbitrary-bit and guard-edge cases."""
+def test_projection_reciprocal_matches_ieee():
+    """The projection reciprocal (icp_kernels.hip proj_rcp_rn) equals IEEE
+    1.0f / den bit for bit for EVERY fp32 den in its guarded range [2^-60,
+    2^60] (exhaustive), and the projected pixel floor(fma(fx x', rz, cx) + 0.5)
+    / in-range decision agrees with the IEEE reciprocal's on 2 x 2^30 random
+    and near-half-integer cases, den inside and outside the guard."""
     for seed in (1, 0x5EED):
         bits, proj = youth_icp.selftest_projdiv(1 << 30, seed)
         assert bits == 0 and proj == 0, (seed, bits, proj)

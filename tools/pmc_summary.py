@@ -19,7 +19,7 @@ def short(name):
 
 def summarize(root):
     out = collections.defaultdict(dict)
-    for f in glob.glob(os.path.join(root, "*", "*counter_collection.csv")):
+    for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         agg = collections.defaultdict(list)
         for r in csv.DictReader(open(f)):
             agg[(short(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))

@@ -59,7 +59,7 @@ def main():
     }
     if "SQ_INSTS_VALU" in r and "GRBM_GUI_ACTIVE" in r:
         simds = 1024
-        for f in glob.glob(os.path.join(root, "*", "*agent_info.csv")):
+        for f in glob.glob(os.path.join(root, "**", "*agent_info.csv"), recursive=True):
             for a in csv.DictReader(open(f)):
                 if a.get("Name", "").startswith("gfx") and a.get("Simd_Count"):
                     simds = int(a["Simd_Count"])
@@ -77,8 +77,8 @@ def main():
             doc["valu_busy_definition"] = ("4 x SQ_ACTIVE_INST_VALU / SIMDs / (GRBM_GUI_ACTIVE / "
                                            "8 XCDs) (rocprof VALUBusy)")
         durs = []
-        for f in glob.glob(os.path.join(root, "*", "*kernel_trace.csv")):
-            if "sq" not in os.path.basename(os.path.dirname(f)):
+        for f in glob.glob(os.path.join(root, "**", "*kernel_trace.csv"), recursive=True):
+            if "pmc_sq" not in f:
                 continue
             for row in csv.DictReader(open(f)):
                 if key in row.get("Kernel_Name", ""):
