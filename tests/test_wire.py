@@ -7,6 +7,11 @@ module: FrameHeader '<IIHHH2xIII' (frameDefinitions.h:11-20), MessageHeader
 of sendDataInChunks (:447-485) and the logger's reassembly rule (:299-354).
 tests/golden/rec_24x16_3f.bin was written by that restatement
 (tests/golden/make_golden.py), not by the C code.
+
+The second half pins the same paths to the REFERENCE itself:
+tests/golden/ref_logger_rec.bin and ref_logger_play.msgs were written by the
+reference's loggingModule.c, compiled unchanged (oracle/Makefile `ref`,
+tests/golden/make_ref_fixtures.py).
 """
 import os
 import struct
@@ -208,3 +213,129 @@ def test_mq_transport_round_trip():
         assert yw.mq_recv_pose(q, 50) is None        # timeout
     finally:
         yw.mq_unlink(q)
+
+
+# ---- pinned to the REFERENCE's own logger ----------------------------------
+# tests/golden/ref_logger_rec.bin / ref_logger_play.msgs were produced by
+# /root/reference/Youth.Source/LoggingModule/loggingModule.c compiled
+# unchanged (oracle/Makefile `ref`, oracle/ref_logger_harness.c,
+# tests/golden/make_ref_fixtures.py): the logger's saveFrameToFile recording
+# of 5 frames (80x60 x3, 24x16, 97x53) and its playback stream
+# (sendMetadata + sendDataInChunks), header bytes 32..291 zeroed (the
+# reference leaves them uninitialised).
+
+REF_REC = os.path.join(GOLDEN, "ref_logger_rec.bin")
+REF_MSGS = os.path.join(GOLDEN, "ref_logger_play.msgs")
+
+
+def _ref_frames():
+    """Frames parsed from the reference recording with struct (independent
+    of the C reader)."""
+    b = open(REF_REC, "rb").read()
+    off, out = 0, []
+    while True:
+        fid, ts, typ, W, H, dn, cn, _ = FH.unpack_from(b, off)
+        off += FH.size
+        if typ == 0xFF:
+            assert off == len(b)
+            return out
+        assert typ == 1 and dn == 2 * W * H and cn == 3 * W * H
+        d = np.frombuffer(b, "<i2", W * H, off).reshape(H, W)
+        c = np.frombuffer(b, np.uint8, cn, off + dn).reshape(H, W, 3)
+        off += dn + cn
+        out.append((fid, ts, d, c))
+
+
+def _ref_msgs():
+    b = open(REF_MSGS, "rb").read()
+    (n,), off, out = struct.unpack_from("<I", b), 4, []
+    for _ in range(n):
+        (ln,) = struct.unpack_from("<I", b, off)
+        out.append(b[off + 4: off + 4 + ln])
+        off += 4 + ln
+    assert off == len(b)
+    return out
+
+
+def test_reference_recording_fixture_shape():
+    fr = _ref_frames()
+    assert [(f[2].shape[1], f[2].shape[0]) for f in fr] == [(80, 60)] * 3 + [(24, 16), (97, 53)]
+    assert [f[0] for f in fr] == [100, 101, 102, 103, 104]
+    assert [f[1] for f in fr] == [1000, 1033, 1066, 1099, 1132]
+    assert min(int(f[2].min()) for f in fr) < 0          # negative depths travel as-is
+
+
+def test_writer_reproduces_reference_recording(tmp_path):
+    """youth_rec_write_frame + youth_rec_close == the reference logger's
+    saveFrameToFile + end marker (loggingModule.c:101-130, 224-226), byte for byte."""
+    p = str(tmp_path / "ours.bin")
+    fr = _ref_frames()
+    assert yw.write_recording(p, fr) == len(fr)
+    assert open(p, "rb").read() == open(REF_REC, "rb").read()
+
+
+def test_reader_reads_reference_recording():
+    got, end = yw.read_recording(REF_REC)
+    assert end == 0
+    fr = _ref_frames()
+    assert len(got) == len(fr)
+    for (h, d, c), (fid, ts, d0, c0) in zip(got, fr):
+        assert (h.frameId, h.timestamp, h.frameType) == (fid, ts, 1)
+        assert (h.width, h.height, h.depthDataSize, h.colorDataSize) == (
+            d0.shape[1], d0.shape[0], d0.nbytes, c0.nbytes)
+        assert np.array_equal(d, d0) and np.array_equal(c, c0)
+
+
+def test_send_frame_reproduces_reference_playback_stream():
+    """youth_wire_send_frame's messages == the reference playback thread's
+    sendMetadata + sendDataInChunks (loggingModule.c:447-502, 584-590), byte
+    for byte (our headers are zero where the reference's are uninitialised)."""
+    ours = [m for fid, ts, d, c in _ref_frames() for m in yw.frame_messages(fid, ts, d, c)]
+    ref = _ref_msgs()
+    assert len(ours) == len(ref) == 23
+    for k, (a, b) in enumerate(zip(ours, ref)):
+        assert a == b, f"message {k} differs"
+
+
+def test_assembler_on_reference_playback_stream():
+    """The reference's playback stream through youth_asm (the logger's rule,
+    colour required, and the ICP rule) yields every recorded frame once."""
+    fr = _ref_frames()
+    for need_color in (True, False):
+        a = yw.Assembler(need_color=need_color)
+        done = [r for m in _ref_msgs() if (r := a.push(m)) is not None]
+        assert len(done) == len(fr)
+        for (h, d, c), (fid, ts, d0, c0) in zip(done, fr):
+            assert (h.frameId, h.timestamp) == (fid, ts)
+            assert np.array_equal(d, d0)
+            # ICP rule: complete at the last depth chunk, before the colour
+            assert np.array_equal(c, c0) if need_color else c is None
+        a.close()
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/Youth.Source/LoggingModule"),
+                    reason="the reference source is only in the build container")
+def test_reference_logger_regenerates_fixtures(tmp_path):
+    """Where the reference is present: rebuild and rerun its logger; its
+    outputs must equal the committed fixtures."""
+    if not yw.mq_available():
+        pytest.skip("POSIX message queues refused here (RLIMIT_MSGQUEUE)")
+    import subprocess
+    import sys
+    sys.path.insert(0, GOLDEN)
+    import make_ref_fixtures as mrf
+    subprocess.run(["make", "-C", os.path.join(os.path.dirname(GOLDEN), "..", "oracle"), "ref"],
+                   check=True, stdout=subprocess.DEVNULL)
+    exe = os.path.join(os.path.dirname(GOLDEN), "..", "oracle", "_ref", "ref_logger")
+    raw = tmp_path / "frames.raw"
+    with open(raw, "wb") as f:
+        fr = mrf.frames()
+        f.write(struct.pack("<I", len(fr)))
+        for fid, ts, d, c in fr:
+            f.write(struct.pack("<4I", fid, ts, d.shape[1], d.shape[0]))
+            f.write(d.astype("<i2").tobytes() + c.tobytes())
+    rec, msgs = tmp_path / "rec.bin", tmp_path / "play.msgs"
+    subprocess.run([exe, str(raw), str(rec), str(msgs)], check=True, timeout=120,
+                   stdout=subprocess.DEVNULL)
+    assert rec.read_bytes() == open(REF_REC, "rb").read()
+    assert msgs.read_bytes() == open(REF_MSGS, "rb").read()
