@@ -135,10 +135,34 @@ int youth_icp_fastdiv_enabled(youth_icp_ctx* ctx);
  * dst are [n_pairs][H][W] int16 host arrays.  T_out: [n_pairs][16] row-major
  * fp32 4x4 with P_dst = T * P_src.  assoc_out: nullable [n_pairs][H*W] int32
  * final-iteration correspondence index (v'*W+u') or -1.  Uses device 0 and a
- * cached context. */
+ * cached context; batches of >= 32 pairs are pipelined in 16-pair chunks
+ * (H2D of chunk k overlaps the align of chunk k-1).  Returns YOUTH_OK even
+ * when a pair's solve was skipped: per-pair status (YOUTH_STATUS_*) is
+ * reported by youth_icp_align_batch_multi's status_out. */
 int youth_icp_align_batch(const int16_t* src, const int16_t* dst, int n_pairs,
                           int W, int H, const youth_intrinsics* K, int iters,
                           float* T_out, int32_t* assoc_out);
+
+/* Multi-GPU host API (SURVEY §8e, C4 from a plain-C host such as main.c): the
+ * n_pairs pairs are split into contiguous shards, one per device
+ * (youth_icp_shard_range: the first n_pairs % k shards get one pair more),
+ * each aligned by its own host thread on its own cached context and stream
+ * (pipelined as youth_icp_align_batch), and every shard's poses land in its
+ * rows of T_out: the pose gather is the per-device D2H into the caller's
+ * buffer, no collective.  devices: nullable list of n_devices distinct device
+ * ids (NULL or n_devices <= 0: every visible device); at most n_pairs devices
+ * are used.  status_out: nullable [n_pairs] int32 YOUTH_STATUS_* per pair
+ * (TIMEOUT folded in).  Blocks until every shard is done; on error returns
+ * the first failing shard's code, youth_icp_last_error naming its device.
+ * Multi-process (one process per GPU, RCCL gather): see INTEGRATION.md. */
+int youth_icp_align_batch_multi(const int16_t* src, const int16_t* dst, int n_pairs,
+                                int W, int H, const youth_intrinsics* K, int iters,
+                                const int* devices, int n_devices, float* T_out,
+                                int32_t* status_out);
+
+/* Shard `part` of n_pairs split over n_parts: *first and *count (the split
+ * youth_icp_align_batch_multi and the bench's ranks use). */
+int youth_icp_shard_range(int n_pairs, int n_parts, int part, int* first, int* count);
 
 /* Context: device workspace sized for max_frames frames of W x H (target
  * records + depth staging); 3 <= W, H <= 16384 and W*H <= 2^26 (EINVAL
@@ -203,6 +227,8 @@ int youth_icp_get_sched_stats(youth_icp_ctx* ctx, unsigned* spins,
  * returns 1 when it ran the small-batch cooperative kernel (k_icp_coop:
  * *workgroups_per_pair x 512 threads, *px_per_lane source pixels per lane,
  * target prep fused), 0 for the persistent batch kernel (k_prep + k_icp),
+ * 2 for the per-iteration fallback (YOUTH_ICP_NO_PERSISTENT=1: k_prep, k_init,
+ * then one k_reduce with the fused last-workgroup solve per iteration),
  * negative on error.  Either pointer may be NULL. */
 int youth_icp_get_plan(youth_icp_ctx* ctx, int* workgroups_per_pair, int* px_per_lane);
 

@@ -36,6 +36,7 @@
 
 #include <mutex>
 #include <string>
+#include <thread>
 #include <algorithm>
 #include <cstdlib>
 #include <vector>
@@ -1849,6 +1850,15 @@ __global__ void k_finish(const double* __restrict__ T64, int n, float* __restric
     if (i == 0 && error && *error) status[t >> 4] |= YOUTH_STATUS_TIMEOUT;
 }
 
+// Per-pair status of one chunk of the host batch API, the launch's timeout
+// flag folded in (as youth_icp_get_poses does).
+__global__ void k_status_out(const int32_t* __restrict__ status, int n,
+                             const unsigned* __restrict__ error, int32_t* __restrict__ out)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) out[t] = status[t] | (*error ? YOUTH_STATUS_TIMEOUT : 0);
+}
+
 }  // namespace
 
 // =============================================================== host side ==
@@ -1917,8 +1927,10 @@ struct youth_icp_ctx {
     int coop_threads = 512;          // YOUTH_ICP_COOP_THREADS=256: one wave per SIMD
     int coop_max_pairs = kCoopMaxPairs;  // YOUTH_ICP_COOP_MAX_PAIRS (<= kCoopMaxPairs)
     int coop_launch = 0;             // YOUTH_ICP_COOP_LAUNCH: 0 serial (default), 1 runtime, 2 plain
+    bool coop_refuse = false;        // YOUTH_ICP_TEST_REFUSE_COOP=1 (test hook)
     int coop_bpc[2][kCoopMaxPx + 1] = {};  // occupancy of k_icp_coop<fast> at npx (LDS)
     unsigned* d_coop = nullptr;      // 2 counter sets of kCoopSetWords
+    int32_t* d_status_out = nullptr; // [max_frames] host batch API: status per pair of the call
     int coop_par = 0;                // set used by the next coop call
     int last_coop_G = 0, last_coop_px = 0;
     bool last_coop = false;          // the last align ran k_icp_coop
@@ -2198,6 +2210,8 @@ static int coop_enqueue(youth_icp_ctx* c, hipStream_t s, void** args, int blocks
     const void* kern = coop_kernel(c->fast, c->coop_threads);
     const dim3 grid((unsigned)blocks), block(c->coop_threads);
     const unsigned lds = (unsigned)coop_lds(npx, c->coop_threads);
+    if (c->coop_refuse)  // test hook: the runtime's refusal, nothing enqueued
+        return set_error(YOUTH_EHIP, "coop_enqueue: cooperative launch refused (test hook)");
     if (c->coop_launch == 1) {
         HIP_TRY(hipLaunchCooperativeKernel(kern, grid, block, args, lds, s));
         return YOUTH_OK;
@@ -2444,7 +2458,7 @@ void youth_icp_destroy(youth_icp_ctx* c)
     void* bufs[] = {c->d_depth, c->d_rec,   c->d_xyz,      c->d_T64, c->d_T32,   c->d_status,
                     c->d_Tinit, c->d_stats, c->d_partials, c->d_neq, c->d_assoc, c->d_Tout,
                     c->d_flag,  c->d_arrivals, c->d_arr_it, c->d_epoch, c->d_head,
-                    c->d_coop};
+                    c->d_coop,  c->d_status_out};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -2547,6 +2561,11 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         if (cpx && atoi(cpx) >= 1 && atoi(cpx) <= kCoopMaxPx) c->coop_px = atoi(cpx);
         const char* cl = getenv("YOUTH_ICP_COOP_LAUNCH");
         c->coop_launch = !cl ? 0 : strcmp(cl, "runtime") == 0 ? 1 : strcmp(cl, "plain") == 0 ? 2 : 0;
+        // test hook (tests/test_gpu_parity.py): every cooperative launch of
+        // this context is refused as the runtime would, exercising the
+        // persistent fallback of run_iterations
+        const char* crf = getenv("YOUTH_ICP_TEST_REFUSE_COOP");
+        c->coop_refuse = crf && *crf && *crf != '0';
         const char* cmp = getenv("YOUTH_ICP_COOP_MAX_PAIRS");
         if (cmp && atoi(cmp) >= 0) c->coop_max_pairs = atoi(cmp);
     }
@@ -2747,7 +2766,7 @@ int youth_icp_get_plan(youth_icp_ctx* c, int* workgroups_per_pair, int* px_per_l
     if (!c) return set_error(YOUTH_EINVAL, "get_plan: null context");
     if (workgroups_per_pair) *workgroups_per_pair = c->last_coop ? c->last_coop_G : 0;
     if (px_per_lane) *px_per_lane = c->last_coop ? c->last_coop_px : 0;
-    return c->last_coop ? 1 : 0;
+    return c->last_coop ? 1 : c->persistent ? 0 : 2;
 }
 
 int youth_icp_get_timing(youth_icp_ctx* c, int kind, double* total_ms, int* launches)
@@ -2841,22 +2860,133 @@ int youth_icp_solve_host(youth_icp_ctx* c, const double* neq, double* T64)
 }
 
 // ----------------------------------------------- one-shot host batch API --
-static std::mutex g_batch_mu;
-static youth_icp_ctx* g_batch_ctx = nullptr;
+// One cached context per device (guarded by that device's mutex), reused while
+// the frame size, intrinsics and capacity fit.
+static std::mutex g_batch_mu[64];
+static youth_icp_ctx* g_batch_ctx[64] = {};
 
 // Pairs per pipelined chunk of the host-buffer batch API (n_pairs: no
 // pipelining).  YOUTH_ICP_BATCH_CHUNK overrides (0 disables).
-static int batch_chunk(int n_pairs, size_t N)
+static int batch_chunk(int n_pairs)
 {
     if (const char* e = getenv("YOUTH_ICP_BATCH_CHUNK")) {
         const int v = atoi(e);
         return v <= 0 ? n_pairs : std::min(v, n_pairs);
     }
-    (void)N;
     // 16-pair chunks run the persistent kernel: copy ~ align.  8-pair chunks
     // (cooperative kernel) ran at 34 K on one box and 20-24 K on another, next to
     // the in-flight copies (profiles/r01/hostio_sweep.txt)
     return n_pairs >= 32 ? 16 : n_pairs;
+}
+
+// Workspace for an align of n_pairs whichever kernel path it takes
+// (cooperative, persistent or per-iteration), so that no hipFree/hipMalloc
+// runs while earlier chunks of a pipelined call are in flight.
+static int reserve_for(youth_icp_ctx* c, int n_pairs)
+{
+    int chunk = 0;
+    const int nb = reduce_geometry(c, n_pairs, &chunk);
+    size_t need = (size_t)nb * n_pairs * kPartStride;
+    int npx = 0, G = 0;
+    if (coop_plan(c, n_pairs, &npx, &G))
+        need = std::max(need, (size_t)2 * n_pairs * G * kPartStride);
+    int rc = ensure_partials(c, need);
+    if (rc) return rc;
+    return ensure_stats(c, c->prm.iters > 0 ? c->prm.iters : 1);
+}
+
+// The host batch align of n_pairs pairs on ONE device: H2D of both depth
+// stacks, align, poses (and per-pair status, nullable) back into the
+// caller's rows.  Batches of >= 32 pairs are pipelined in chunks: chunk k's
+// H2D on a transfer stream overlaps the align of chunk k-1 (every chunk has
+// its own device frames, so nothing is reused inside one call).  On any error
+// both streams are drained before returning, so no copy still reads the
+// caller's buffers.  Caller holds g_batch_mu[dev].
+static int batch_on_device(int dev, const int16_t* src, const int16_t* dst, int n_pairs, int W,
+                           int H, const youth_intrinsics& Kd, int iters, float* T_out,
+                           int32_t* status_out, int32_t* assoc_out)
+{
+    youth_icp_params P = youth_default_params();
+    P.iters = iters;
+    youth_icp_ctx*& slot = g_batch_ctx[dev];
+    youth_icp_ctx* c = slot;
+    const bool same = c && c->W == W && c->H == H && c->max_frames >= 2 * n_pairs &&
+                      c->K.fx == Kd.fx && c->K.fy == Kd.fy && c->K.cx == Kd.cx &&
+                      c->K.cy == Kd.cy && c->K.ds == Kd.depth_scale;
+    if (!same) {
+        if (c) youth_icp_destroy(c);
+        slot = nullptr;
+        c = youth_icp_create(dev, W, H, 2 * n_pairs, &Kd, &P);
+        if (!c)
+            return g_last_error.find("no HIP device") != std::string::npos ? YOUTH_ENODEV
+                                                                          : YOUTH_EHIP;
+        slot = c;
+    }
+    c->prm = P;
+    int rc = bind_device(c);
+    if (rc) return rc;
+    hipStream_t s = c->stream;
+    if (!c->xfer) HIP_TRY(hipStreamCreateWithFlags(&c->xfer, hipStreamNonBlocking));
+    if (status_out && !c->d_status_out)
+        HIP_TRY(hipMalloc(&c->d_status_out, (size_t)c->max_frames * sizeof(int32_t)));
+    auto drain = [c, s](int code) {
+        (void)hipStreamSynchronize(c->xfer);
+        (void)hipStreamSynchronize(s);
+        return code;
+    };
+    const size_t N = c->N;
+    int16_t* d_s = c->d_depth;
+    int16_t* d_d = c->d_depth + (size_t)n_pairs * N;
+    const int chunk = assoc_out ? n_pairs : batch_chunk(n_pairs);
+    const int n_chunks = (n_pairs + chunk - 1) / chunk;
+    rc = reserve_for(c, chunk);
+    if (!rc && n_pairs % chunk) rc = reserve_for(c, n_pairs % chunk);
+    if (rc) return rc;
+    while ((int)c->xfer_ev.size() < n_chunks) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->xfer_ev.push_back(e);
+    }
+    for (int k = 0; k < n_chunks; ++k) {
+        const size_t p0 = (size_t)k * chunk;
+        const int cnt = (int)std::min<size_t>(chunk, n_pairs - p0);
+        const size_t bytes = (size_t)cnt * N * sizeof(int16_t);
+        hipError_t e = hipMemcpyAsync(d_s + p0 * N, src + p0 * N, bytes, hipMemcpyHostToDevice,
+                                      c->xfer);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(d_d + p0 * N, dst + p0 * N, bytes, hipMemcpyHostToDevice, c->xfer);
+        if (e == hipSuccess) e = hipEventRecord(c->xfer_ev[k], c->xfer);
+        if (e == hipSuccess) e = hipStreamWaitEvent(s, c->xfer_ev[k], 0);
+        if (e != hipSuccess)
+            return drain(set_error(YOUTH_EHIP, "align_batch: %s", hipGetErrorString(e)));
+        rc = youth_icp_align_pairs_device(c, d_s + p0 * N, d_d + p0 * N, cnt, nullptr,
+                                          c->d_Tout + p0 * 16, s);
+        if (rc) return drain(rc);
+        if (status_out) {
+            hipLaunchKernelGGL(k_status_out, dim3((cnt + 255) / 256), dim3(256), 0, s,
+                               c->d_status, cnt, (const unsigned*)(c->d_head + kQError),
+                               c->d_status_out + p0);
+            if ((e = hipGetLastError()) != hipSuccess)
+                return drain(set_error(YOUTH_EHIP, "align_batch: %s", hipGetErrorString(e)));
+        }
+    }
+    if (assoc_out) {
+        int nb = 0;
+        rc = launch_reduce(c, s, d_s, PairMap{0, 0}, n_pairs, true, &nb);
+        if (rc) return drain(rc);
+        hipError_t e = hipMemcpyAsync(assoc_out, c->d_assoc, (size_t)n_pairs * N * sizeof(int32_t),
+                                      hipMemcpyDeviceToHost, s);
+        if (e != hipSuccess)
+            return drain(set_error(YOUTH_EHIP, "align_batch: %s", hipGetErrorString(e)));
+    }
+    hipError_t e = hipMemcpyAsync(T_out, c->d_Tout, (size_t)n_pairs * 16 * sizeof(float),
+                                  hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess && status_out)
+        e = hipMemcpyAsync(status_out, c->d_status_out, (size_t)n_pairs * sizeof(int32_t),
+                           hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) return drain(set_error(YOUTH_EHIP, "align_batch: %s", hipGetErrorString(e)));
+    HIP_TRY(hipStreamSynchronize(s));
+    return YOUTH_OK;
 }
 
 int youth_icp_align_batch(const int16_t* src, const int16_t* dst, int n_pairs, int W, int H,
@@ -2865,77 +2995,73 @@ int youth_icp_align_batch(const int16_t* src, const int16_t* dst, int n_pairs, i
 {
     if (!src || !dst || n_pairs <= 0 || W < 3 || H < 3 || iters < 0 || !T_out)
         return set_error(YOUTH_EINVAL, "align_batch: bad arguments %d", n_pairs);
-    std::lock_guard<std::mutex> lk(g_batch_mu);
+    std::lock_guard<std::mutex> lk(g_batch_mu[0]);
     const youth_intrinsics Kd = K ? *K : youth_default_intrinsics(W, H);
-    youth_icp_params P = youth_default_params();
-    P.iters = iters;
-    youth_icp_ctx* c = g_batch_ctx;
-    const bool same = c && c->W == W && c->H == H && c->max_frames >= 2 * n_pairs &&
-                      c->K.fx == Kd.fx && c->K.fy == Kd.fy && c->K.cx == Kd.cx &&
-                      c->K.cy == Kd.cy && c->K.ds == Kd.depth_scale;
-    if (!same) {
-        if (c) youth_icp_destroy(c);
-        g_batch_ctx = nullptr;
-        c = youth_icp_create(0, W, H, 2 * n_pairs, &Kd, &P);
-        if (!c)
-            return g_last_error.find("no HIP device") != std::string::npos ? YOUTH_ENODEV
-                                                                          : YOUTH_EHIP;
-        g_batch_ctx = c;
-    }
-    c->prm = P;
-    int rc = bind_device(c);
-    if (rc) return rc;
-    hipStream_t s = c->stream;
-    const size_t N = c->N;
-    int16_t* d_s = c->d_depth;
-    int16_t* d_d = c->d_depth + (size_t)n_pairs * N;
-    const int chunk = assoc_out ? n_pairs : batch_chunk(n_pairs, N);
-    if (chunk < n_pairs) {
-        // pipelined: chunk k's depth goes up on the transfer stream while the
-        // align of chunk k-1 runs on the compute stream (every chunk has its
-        // own device frames, so no buffer is reused inside one call)
-        if (!c->xfer) HIP_TRY(hipStreamCreateWithFlags(&c->xfer, hipStreamNonBlocking));
-        const int n_chunks = (n_pairs + chunk - 1) / chunk;
-        while ((int)c->xfer_ev.size() < n_chunks) {
-            hipEvent_t e;
-            HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            c->xfer_ev.push_back(e);
+    return batch_on_device(0, src, dst, n_pairs, W, H, Kd, iters, T_out, nullptr, assoc_out);
+}
+
+// Contiguous shard [first, first + count) of n pairs for part r of k (the
+// first n % k parts get one more), as youth_dist.pair_range on the bench side.
+static void shard_range(int n, int k, int r, int* first, int* count)
+{
+    const int q = n / k, m = n % k;
+    *first = r * q + std::min(r, m);
+    *count = q + (r < m ? 1 : 0);
+}
+
+int youth_icp_shard_range(int n_pairs, int n_parts, int part, int* first, int* count)
+{
+    if (n_pairs < 0 || n_parts <= 0 || part < 0 || part >= n_parts || !first || !count)
+        return set_error(YOUTH_EINVAL, "shard_range: bad arguments");
+    shard_range(n_pairs, n_parts, part, first, count);
+    return YOUTH_OK;
+}
+
+int youth_icp_align_batch_multi(const int16_t* src, const int16_t* dst, int n_pairs, int W,
+                                int H, const youth_intrinsics* K, int iters, const int* devices,
+                                int n_devices, float* T_out, int32_t* status_out)
+{
+    if (!src || !dst || n_pairs <= 0 || W < 3 || H < 3 || iters < 0 || !T_out)
+        return set_error(YOUTH_EINVAL, "align_batch_multi: bad arguments %d", n_pairs);
+    const int ndev = youth_icp_device_count();
+    if (ndev <= 0) return set_error(YOUTH_ENODEV, "align_batch_multi: no HIP device");
+    std::vector<int> devs;
+    if (devices && n_devices > 0) {
+        for (int i = 0; i < n_devices; ++i) {
+            if (devices[i] < 0 || devices[i] >= ndev || devices[i] >= 64)
+                return set_error(YOUTH_EINVAL, "align_batch_multi: no HIP device %d", devices[i]);
+            if (std::find(devs.begin(), devs.end(), devices[i]) != devs.end())
+                return set_error(YOUTH_EINVAL, "align_batch_multi: device %d listed twice",
+                                 devices[i]);
+            devs.push_back(devices[i]);
         }
-        for (int k = 0; k < n_chunks; ++k) {
-            const size_t p0 = (size_t)k * chunk;
-            const int cnt = (int)std::min<size_t>(chunk, n_pairs - p0);
-            const size_t bytes = (size_t)cnt * N * sizeof(int16_t);
-            HIP_TRY(hipMemcpyAsync(d_s + p0 * N, src + p0 * N, bytes, hipMemcpyHostToDevice,
-                                   c->xfer));
-            HIP_TRY(hipMemcpyAsync(d_d + p0 * N, dst + p0 * N, bytes, hipMemcpyHostToDevice,
-                                   c->xfer));
-            HIP_TRY(hipEventRecord(c->xfer_ev[k], c->xfer));
-            HIP_TRY(hipStreamWaitEvent(s, c->xfer_ev[k], 0));
-            rc = youth_icp_align_pairs_device(c, d_s + p0 * N, d_d + p0 * N, cnt, nullptr,
-                                              c->d_Tout + p0 * 16, s);
-            if (rc) return rc;
+    } else {
+        for (int d = 0; d < std::min(ndev, 64); ++d) devs.push_back(d);
+    }
+    const int parts = std::min((int)devs.size(), n_pairs);
+    const youth_intrinsics Kd = K ? *K : youth_default_intrinsics(W, H);
+    const size_t N = (size_t)W * H;
+    std::vector<int> rcs(parts, YOUTH_OK);
+    std::vector<std::string> errs(parts);
+    auto work = [&](int r) {
+        int first = 0, cnt = 0;
+        shard_range(n_pairs, parts, r, &first, &cnt);
+        std::lock_guard<std::mutex> lk(g_batch_mu[devs[r]]);
+        rcs[r] = batch_on_device(devs[r], src + (size_t)first * N, dst + (size_t)first * N, cnt, W,
+                                 H, Kd, iters, T_out + (size_t)first * 16,
+                                 status_out ? status_out + first : nullptr, nullptr);
+        if (rcs[r]) errs[r] = g_last_error;  // thread-local: carried to the caller below
+    };
+    // one host thread per device; shard 0 runs on the calling thread
+    std::vector<std::thread> th;
+    for (int r = 1; r < parts; ++r) th.emplace_back(work, r);
+    work(0);
+    for (auto& t : th) t.join();
+    for (int r = 0; r < parts; ++r)
+        if (rcs[r]) {
+            g_last_error = "device " + std::to_string(devs[r]) + ": " + errs[r];
+            return rcs[r];
         }
-        HIP_TRY(hipMemcpyAsync(T_out, c->d_Tout, (size_t)n_pairs * 16 * sizeof(float),
-                               hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        return YOUTH_OK;
-    }
-    HIP_TRY(hipMemcpyAsync(d_s, src, (size_t)n_pairs * N * sizeof(int16_t), hipMemcpyHostToDevice,
-                           s));
-    HIP_TRY(hipMemcpyAsync(d_d, dst, (size_t)n_pairs * N * sizeof(int16_t), hipMemcpyHostToDevice,
-                           s));
-    rc = youth_icp_align_pairs_device(c, d_s, d_d, n_pairs, nullptr, c->d_Tout, s);
-    if (rc) return rc;
-    if (assoc_out) {
-        int nb = 0;
-        rc = launch_reduce(c, s, d_s, PairMap{0, 0}, n_pairs, true, &nb);
-        if (rc) return rc;
-        HIP_TRY(hipMemcpyAsync(assoc_out, c->d_assoc, (size_t)n_pairs * N * sizeof(int32_t),
-                               hipMemcpyDeviceToHost, s));
-    }
-    HIP_TRY(hipMemcpyAsync(T_out, c->d_Tout, (size_t)n_pairs * 16 * sizeof(float),
-                           hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
     return YOUTH_OK;
 }
 

@@ -85,6 +85,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "youth_icp_fastdiv_enabled": (c_int, [c_void_p]),
         "youth_icp_align_batch": (c_int, [P16, P16, c_int, c_int, c_int, POINTER(Intrinsics),
                                           c_int, PF, PI32]),
+        "youth_icp_align_batch_multi": (c_int, [P16, P16, c_int, c_int, c_int,
+                                                POINTER(Intrinsics), c_int, PI32, c_int, PF,
+                                                PI32]),
+        "youth_icp_shard_range": (c_int, [c_int, c_int, c_int, POINTER(c_int), POINTER(c_int)]),
         "youth_icp_create": (c_void_p, [c_int, c_int, c_int, c_int, POINTER(Intrinsics),
                                         POINTER(Params)]),
         "youth_icp_destroy": (None, [c_void_p]),
@@ -375,6 +379,8 @@ class IcpContext:
         if r == 1:
             return {"kernel": "k_icp_coop", "workgroups_per_pair": g.value, "threads": 512,
                     "px_per_lane": px.value}
+        if r == 2:
+            return {"kernel": "k_prep + k_init + k_reduce x iters (per-iteration)"}
         return {"kernel": "k_prep + k_icp (persistent)"}
 
     # host-array stage entry points (parity tests)
@@ -452,3 +458,32 @@ def align_batch(src: np.ndarray, dst: np.ndarray, K: Intrinsics | None = None, i
     _check(lib.youth_icp_align_batch(_p(s, c_int16), _p(d, c_int16), n, W, H, Kp, iters,
                                      _p(T, c_float), _p(assoc, c_int32)))
     return T, assoc
+
+
+def align_batch_multi(src: np.ndarray, dst: np.ndarray, K: Intrinsics | None = None,
+                      iters: int = 10, devices=None):
+    """youth_icp_align_batch_multi: contiguous pair shards over `devices`
+    (None: every visible device), one host thread each -> (T [n,4,4] fp32,
+    status [n] int32)."""
+    s = np.ascontiguousarray(src, np.int16)
+    d = np.ascontiguousarray(dst, np.int16)
+    if s.ndim == 2:
+        s, d = s[None], d[None]
+    n, H, W = s.shape
+    T = np.zeros((n, 4, 4), np.float32)
+    st = np.zeros(n, np.int32)
+    dv = None if devices is None else np.ascontiguousarray(devices, np.int32)
+    lib = load_library()
+    Kp = ctypes.byref(K) if K is not None else None
+    _check(lib.youth_icp_align_batch_multi(_p(s, c_int16), _p(d, c_int16), n, W, H, Kp, iters,
+                                           _p(dv, c_int32), 0 if dv is None else len(dv),
+                                           _p(T, c_float), _p(st, c_int32)))
+    return T, st
+
+
+def shard_range(n_pairs: int, n_parts: int, part: int):
+    """youth_icp_shard_range -> (first, count)."""
+    f, c = c_int(0), c_int(0)
+    _check(load_library().youth_icp_shard_range(n_pairs, n_parts, part, ctypes.byref(f),
+                                                ctypes.byref(c)))
+    return f.value, c.value

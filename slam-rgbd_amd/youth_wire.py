@@ -226,8 +226,38 @@ def _libc_mq():
     return libc
 
 
+def mq_raise_limit() -> None:
+    """Raise the soft RLIMIT_MSGQUEUE to the hard limit (a queue with the
+    reference's attributes, 10 x 8192 B, needs ~82 KB of it)."""
+    import resource
+    soft, hard = resource.getrlimit(resource.RLIMIT_MSGQUEUE)
+    if hard == resource.RLIM_INFINITY or soft < hard:
+        try:
+            resource.setrlimit(resource.RLIMIT_MSGQUEUE, (hard, hard))
+        except (ValueError, OSError):
+            pass
+
+
+def mq_diagnose() -> str:
+    """Why a queue with the reference's attributes cannot be opened: errno of
+    the probe, RLIMIT_MSGQUEUE and the /proc/sys/fs/mqueue limits."""
+    import resource
+    parts = [f"rlimit_msgqueue={resource.getrlimit(resource.RLIMIT_MSGQUEUE)}"]
+    for k in ("msg_max", "msgsize_max", "queues_max"):
+        try:
+            parts.append(f"{k}={open('/proc/sys/fs/mqueue/' + k).read().strip()}")
+        except OSError as e:
+            parts.append(f"{k}=?({e.errno})")
+    parts.append(f"probe_errno={_probe()[1]}")
+    return ", ".join(parts)
+
+
 def mq_available() -> bool:
     """POSIX queues usable here (RLIMIT_MSGQUEUE may be 0 for the user)."""
+    return _probe()[0]
+
+
+def _probe():
     class Attr(Structure):
         _fields_ = [("flags", ctypes.c_long), ("maxmsg", ctypes.c_long),
                     ("msgsize", ctypes.c_long), ("curmsgs", ctypes.c_long),
@@ -239,10 +269,10 @@ def mq_available() -> bool:
     a = Attr(0, 10, MAX_MSG_SIZE, 0)
     fd = libc.mq_open(name, os.O_CREAT | os.O_RDWR, 0o600, ctypes.byref(a))
     if fd < 0:
-        return False
+        return False, ctypes.get_errno()
     libc.mq_close(fd)
     libc.mq_unlink(name)
-    return True
+    return True, 0
 
 
 def mq_unlink(name: str) -> None:

@@ -76,6 +76,9 @@ def test_no_device_fails_loudly(has_gpu):
     src = np.ones((1, 48, 64), np.int16)
     with pytest.raises(youth_icp.IcpError):
         youth_icp.align_batch(src, src)
+    with pytest.raises(youth_icp.IcpError) as e:
+        youth_icp.align_batch_multi(src, src)
+    assert e.value.code == youth_icp.YOUTH_ENODEV
     # SLAM.h API: the module refuses to start, so frames are rejected (return 0)
     youth_icp.initSlamModule(None)
     assert youth_icp.isSlamModuleRunning() == 0
@@ -89,6 +92,25 @@ def test_no_device_fails_loudly(has_gpu):
     with pytest.raises(youth_icp.IcpError) as e:
         youth_viewer.CloudBuilder(64, 48)
     assert e.value.code == youth_icp.YOUTH_ENODEV
+
+
+def test_shard_range_matches_bench_split():
+    """youth_icp_shard_range (the multi-GPU host API's split) == the bench
+    ranks' youth_dist.pair_range, and the shards tile [0, n) contiguously."""
+    import youth_dist
+    for n in (1, 2, 7, 64, 511, 512, 999):
+        for k in (1, 2, 3, 4, 8):
+            nxt = 0
+            for r in range(k):
+                f, c = youth_icp.shard_range(n, k, r)
+                assert (f, c) == youth_dist.pair_range(n, k, r)
+                assert f == nxt and c >= 0
+                nxt = f + c
+            assert nxt == n
+    with pytest.raises(youth_icp.IcpError):
+        youth_icp.shard_range(8, 0, 0)
+    with pytest.raises(youth_icp.IcpError):
+        youth_icp.shard_range(8, 2, 2)
 
 
 def test_queue_overflow_policy_matches_reference():

@@ -166,6 +166,48 @@ def test_align_batch_pipelined_chunks(chunk, monkeypatch):
         assert _pose_err(T_chk[p], T64) <= POSE_TOL, p
 
 
+def test_align_batch_default_chunks_ragged_tail(monkeypatch):
+    """Default pipelining at 40 pairs: chunks of 16, 16 and 8 (persistent
+    kernel, then a cooperative tail on the same context, workspace reserved
+    for both before the loop) equal the unpipelined call bit for bit and the
+    oracle within 1e-5."""
+    n = 40
+    src, dst, _ = youth_synth.pairs(200, n)
+    monkeypatch.delenv("YOUTH_ICP_BATCH_CHUNK", raising=False)
+    T_chk, _ = youth_icp.align_batch(src, dst, iters=10)
+    monkeypatch.setenv("YOUTH_ICP_BATCH_CHUNK", "0")
+    T_one, _ = youth_icp.align_batch(src, dst, iters=10)
+    assert np.array_equal(T_chk, T_one)
+    for p in (0, 15, 16, 32, 39):
+        T64, _, st, _ = oracle.align(src[p], dst[p], iters=10)
+        assert st == 0 and _pose_err(T_chk[p], T64) <= POSE_TOL, p
+
+
+@pytest.mark.parametrize("devices", [None, [0]])
+def test_align_batch_multi_matches_single_device(devices):
+    """youth_icp_align_batch_multi (one host thread + context per device,
+    contiguous shards, poses written into the caller's rows) on this box's
+    device(s): poses equal youth_icp_align_batch's bit for bit, the oracle's
+    within 1e-5, and per-pair status reported (a pair without source pixels
+    is YOUTH_STATUS_FEW_MATCHES with the identity pose).  N > 1 devices:
+    unmeasured here (one-GPU boxes)."""
+    n = 37
+    src, dst, _ = youth_synth.pairs(400, n, 160, 120)
+    src[5] = 0
+    T_m, st = youth_icp.align_batch_multi(src, dst, iters=10, devices=devices)
+    T_1, _ = youth_icp.align_batch(src, dst, iters=10)
+    assert np.array_equal(T_m, T_1)
+    assert st[5] == youth_icp.STATUS_FEW_MATCHES and np.array_equal(T_m[5], np.eye(4))
+    assert not np.delete(st, 5).any()
+    for p in (0, 6, 36):
+        T64, _, sto, _ = oracle.align(src[p], dst[p], iters=10)
+        assert sto == 0 and _pose_err(T_m[p], T64) <= POSE_TOL, p
+    with pytest.raises(youth_icp.IcpError):
+        youth_icp.align_batch_multi(src, dst, devices=[0, 0])
+    with pytest.raises(youth_icp.IcpError):
+        youth_icp.align_batch_multi(src, dst, devices=[youth_icp.device_count()])
+
+
 @pytest.mark.parametrize("n", [1, 40])
 def test_large_step_rodrigues_branch(n):
     """Spec a10 above theta = 5 deg (theta^2 >= 2^-7): the SE(3) update leaves
@@ -285,6 +327,36 @@ def test_sequence_api_matches_oracle():
         T64, _, st = ctx.get_poses(n - 1)
     for k in range(n - 1):
         assert _pose_err(T64[k], g["T_rel"][k]) <= POSE_TOL, k
+
+
+def test_sequence_c5_workload_640x480():
+    """Config C5 at its frame size: a 201-frame 640x480 synthetic sequence
+    (seed 0x5EED1000) through align_sequence_device (every frame
+    prepared once, 200 relative poses in one call).  EVERY relative pose
+    within 1e-5 of the oracle (OpenMP over pairs); per-iteration
+    correspondence counts equal to the oracle's and association indices at
+    the final pose bit-exact on sampled pairs."""
+    import torch
+    F = 201
+    frames, _ = youth_synth.sequence(0, F)
+    d = torch.from_numpy(frames).cuda()
+    torch.cuda.synchronize()
+    with youth_icp.IcpContext(640, 480, F - 1) as ctx:
+        ctx.align_sequence_device(d.data_ptr(), F)
+        ctx.sync()
+        T64, T32, st = ctx.get_poses(F - 1)
+        cnt, _ = ctx.get_stats(F - 1, 10)
+        T_cpu, st_cpu = oracle.align_batch(frames[1:], frames[:-1], iters=10,
+                                           n_threads=min(16, os.cpu_count() or 1))
+        assert np.array_equal(st, st_cpu) and not st.any()
+        err = [_pose_err(T64[k], T_cpu[k]) for k in range(F - 1)]
+        assert max(err) <= POSE_TOL, int(np.argmax(err))
+        K = oracle.viewer_K(640, 480)
+        for k in (0, 1, 77, 150, F - 2):
+            _, _, _, stats = oracle.align(frames[k + 1], frames[k], iters=10)
+            assert np.array_equal(cnt[k], stats[:, 0]), k
+            g_idx, _ = ctx.reduce(frames[k + 1], frames[k], T32[k][:3])
+            assert np.array_equal(g_idx, oracle.associate(frames[k + 1], frames[k], T32[k][:3], K))
 
 
 def test_track_frame_matches_oracle():
@@ -446,14 +518,29 @@ def test_plain_c_host_demo(tmp_path):
     assert np.allclose(rows[-1, 1:4], acc[:3, 3], atol=1e-6)
 
 
-@pytest.mark.parametrize("mode", ["coop", "persistent"])
+PLAN = {"coop": "k_icp_coop", "persistent": "k_prep + k_icp (persistent)",
+        "coop_refused": "k_prep + k_icp (persistent)",
+        "per_iteration": "k_prep + k_init + k_reduce x iters (per-iteration)"}
+
+
+@pytest.mark.parametrize("mode", ["coop", "persistent", "coop_refused", "per_iteration"])
 def test_kernel_paths_match_oracle(monkeypatch, mode):
-    """Both kernel paths of an align give the oracle's pose (<= 1e-5) and the
+    """Every kernel path of an align gives the oracle's pose (<= 1e-5) and the
     oracle's per-iteration correspondence counts, on repeated calls: the
-    small-batch cooperative kernel (k_icp_coop, fused prep) and the persistent
-    batch kernel (k_prep + k_icp)."""
+    small-batch cooperative kernel (k_icp_coop, fused prep); the persistent
+    batch kernel (k_prep + k_icp); the persistent fallback taken when the
+    runtime refuses the cooperative launch (forced by the
+    YOUTH_ICP_TEST_REFUSE_COOP hook with the runtime launch path); and the
+    per-iteration fallback (YOUTH_ICP_NO_PERSISTENT=1: k_reduce with the fused
+    last-workgroup solve, once per iteration)."""
     if mode == "persistent":
         monkeypatch.setenv("YOUTH_ICP_NO_COOP", "1")
+    if mode == "coop_refused":
+        monkeypatch.setenv("YOUTH_ICP_COOP_LAUNCH", "runtime")
+        monkeypatch.setenv("YOUTH_ICP_TEST_REFUSE_COOP", "1")
+    if mode == "per_iteration":
+        monkeypatch.setenv("YOUTH_ICP_NO_COOP", "1")
+        monkeypatch.setenv("YOUTH_ICP_NO_PERSISTENT", "1")
     n = 3
     src, dst, _ = youth_synth.pairs(40, n)
     import torch
@@ -468,8 +555,7 @@ def test_kernel_paths_match_oracle(monkeypatch, mode):
         plan = ctx.get_plan()
         T64, T32, st = ctx.get_poses(n)
         cnt, _ = ctx.get_stats(n, 10)
-    assert plan["kernel"] == ("k_icp_coop" if mode == "coop" else
-                              "k_prep + k_icp (persistent)")
+    assert plan["kernel"] == PLAN[mode]
     Tdev = out.cpu().numpy().reshape(n, 4, 4)
     for p in range(n):
         T64o, _, sto, stats = oracle.align(src[p], dst[p], iters=10)
@@ -526,3 +612,22 @@ def test_max_frame_size_8192x8192():
     idx = oracle.associate(src[0], dst[0], Tg[0][:3], K)
     assert int((idx >= 0).sum()) > W * H // 4
     assert np.array_equal(assoc[0], idx)
+
+
+def test_plain_c_batch_multi_demo(tmp_path):
+    """youth_icp_align_batch_multi driven from plain C99 over every visible
+    device (examples/batch_multi_demo.c): every pose within 1e-5 of the
+    oracle."""
+    import subprocess
+    from conftest import PKG
+    n, W, H = 6, 320, 240
+    out = str(tmp_path / "T.f32")
+    r = subprocess.run([os.path.join(PKG, "batch_multi_demo"), str(n), out, str(W), str(H)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    T = np.fromfile(out, np.float32).reshape(n, 4, 4)
+    src, dst, _ = youth_synth.pairs(0, n, W, H)
+    T_cpu, st = oracle.align_batch(src, dst, iters=10, n_threads=min(n, os.cpu_count() or 1))
+    assert not st.any()
+    for p in range(n):
+        assert _pose_err(T[p], T_cpu[p]) <= POSE_TOL, p

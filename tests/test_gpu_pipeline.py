@@ -92,8 +92,12 @@ def test_algorithm_loop_in_process():
 
 
 def test_algorithm_loop_over_queues():
+    # the reference's queue attributes (10 x 8192 B, sensorModule.c:73-77,
+    # loggingModule.c:138-141) need ~82 KB of RLIMIT_MSGQUEUE per queue:
+    # raise the soft limit to the hard one first
+    youth_wire.mq_raise_limit()
     if not youth_wire.mq_available():
-        pytest.skip("POSIX message queues refused here (RLIMIT_MSGQUEUE)")
+        pytest.skip("POSIX message queues refused here: " + youth_wire.mq_diagnose())
     fq = f"/youth_t_frames_{os.getpid()}"
     pq = f"/youth_t_poses_{os.getpid()}"
     L = youth_wire.lib()
