@@ -156,8 +156,10 @@ typedef int (*youth_msg_source)(void* user, void* buf, size_t cap, int timeout_m
 /* The frame loop over any transport: pull messages from `recv`, reassemble
  * frames, processSlamFrame() each one, and hand every new trajectory pose to
  * `publish` (NULL: none) as one YOUTH_MSG_TYPE_POSE message.  Runs until recv
- * returns < 0, *stop becomes non-zero or the SLAM module stops.  Returns the
- * number of frames handed to processSlamFrame. */
+ * returns < 0, *stop becomes non-zero or the SLAM module stops.  *stop is
+ * read with an atomic acquire load: set it from another thread with an
+ * atomic store (e.g. __atomic_store_n(stop, 1, __ATOMIC_RELEASE)).  Returns
+ * the number of frames handed to processSlamFrame. */
 int youth_algorithm_run(youth_msg_source recv, void* recv_user, youth_msg_sink publish,
                         void* publish_user, volatile int* stop);
 

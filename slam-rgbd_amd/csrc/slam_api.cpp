@@ -153,6 +153,7 @@ struct PoseRec {
 };
 
 std::mutex g_slam_mu;  // SLAM.cpp:16 slam_mutex: tracker + trajectory
+std::mutex g_life_mu;  // initSlamModule / stopSlamModule against each other
 std::atomic<bool> g_running{false};
 std::atomic<bool> g_process{false};  // SLAM.cpp:29 process_frames
 std::atomic<bool> g_busy{false};
@@ -324,6 +325,9 @@ void initSlamModule(const char* config_file, const char* vocabulary_file)
 {
     (void)vocabulary_file;  // no ORB vocabulary in an ICP tracker
     fprintf(stderr, "youth_icp: initializing HIP ICP module...\n");
+    // g_life_mu serialises init/stop (SLAM.cpp:69 takes slam_mutex): two
+    // concurrent inits must not both start a worker
+    std::lock_guard<std::mutex> life(g_life_mu);
     if (g_running.load()) {
         fprintf(stderr, "youth_icp: SLAM module is already running\n");
         return;
@@ -370,6 +374,7 @@ void initSlamModule(const char* config_file, const char* vocabulary_file)
 void stopSlamModule(void)
 {
     fprintf(stderr, "youth_icp: stopping HIP ICP module...\n");
+    std::lock_guard<std::mutex> life(g_life_mu);
     g_process.store(false);
     if (g_worker.joinable()) g_worker.join();
     if (g_queue) youth_queue_clear(g_queue);

@@ -355,7 +355,9 @@ int youth_algorithm_run(youth_msg_source recv, void* recv_user, youth_msg_sink p
     uint32_t ring_ts[TS_RING];
     int ring_id[TS_RING];
     int ring_n = 0, frames = 0, published = 0;
-    while (!(stop && *stop) && isSlamModuleRunning()) {
+    /* *stop is written by another thread: read it atomically (the writer
+     * should store atomically too, youth_wire.h) */
+    while (!(stop && __atomic_load_n(stop, __ATOMIC_ACQUIRE)) && isSlamModuleRunning()) {
         const int n = recv(recv_user, buf, YOUTH_MAX_MSG_SIZE, 50);
         if (n < 0) break;
         if (n > 0) {

@@ -1,0 +1,61 @@
+/*
+ * icp_stub.c — TEST INFRASTRUCTURE ONLY: a CPU stand-in for the six
+ * libyouth_icp device entry points the host-side threading code calls
+ * (slam_api.cpp's worker: create / destroy / track_frame / track_reset /
+ * device_count / last_error, plus youth_default_intrinsics), so the SLAM.h
+ * queue + worker, the AlgorithmModule frame loop and the POSIX-queue
+ * transport can run under ThreadSanitizer / AddressSanitizer on a machine
+ * without a GPU (SURVEY §5 "Race detection").  It is linked only into the
+ * sanitizer driver (tests/tsan/Makefile), never into libyouth_icp.so, and
+ * computes no ICP: the "relative pose" is a translation derived from the
+ * frame's depth sum, enough for the driver to check that every frame reached
+ * the trajectory in order.
+ */
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "youth_icp.h"
+
+struct youth_icp_ctx {
+    int W, H, has_ref;
+    long long ref_sum;
+};
+
+int youth_icp_device_count(void) { return 1; }
+const char* youth_icp_last_error(void) { return "stub"; }
+
+youth_intrinsics youth_default_intrinsics(int width, int height)
+{
+    youth_intrinsics K = {570.3f, 570.3f, (float)(width / 2), (float)(height / 2), 1000.0f};
+    return K;
+}
+
+youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
+                                const youth_intrinsics* K, const youth_icp_params* P)
+{
+    (void)device, (void)max_frames, (void)K, (void)P;
+    youth_icp_ctx* c = (youth_icp_ctx*)calloc(1, sizeof(*c));
+    if (c) c->W = W, c->H = H;
+    return c;
+}
+
+void youth_icp_destroy(youth_icp_ctx* c) { free(c); }
+void youth_icp_track_reset(youth_icp_ctx* c) { c->has_ref = 0; }
+
+int youth_icp_track_frame(youth_icp_ctx* c, const int16_t* depth, const double* T_init,
+                          double* T_rel, int* has_ref)
+{
+    (void)T_init;
+    long long s = 0;
+    for (int i = 0; i < c->W * c->H; ++i) s += depth[i];
+    struct timespec ts = {0, 200 * 1000};  /* a GPU align takes ~100 us */
+    nanosleep(&ts, NULL);
+    memset(T_rel, 0, 16 * sizeof(double));
+    T_rel[0] = T_rel[5] = T_rel[10] = T_rel[15] = 1.0;
+    if (has_ref) *has_ref = c->has_ref;
+    if (c->has_ref) T_rel[3] = (double)(s - c->ref_sum) * 1e-6;
+    c->has_ref = 1;
+    c->ref_sum = s;
+    return 0;
+}
