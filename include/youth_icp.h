@@ -125,7 +125,7 @@ const char* youth_icp_last_error(void);
 /* Number of visible HIP devices (0 when none; never fails). */
 int youth_icp_device_count(void);
 
-/* 1 when this context's back-projection divides use the 3-instruction
+/* 1 when this context's back-projection divides use the 2-instruction
  * sequence (proven equal to IEEE division on the whole pixel x depth domain
  * by an on-device exhaustive check at creation), 0 for the IEEE path.
  * Environment YOUTH_ICP_NO_FASTDIV=1 forces the IEEE path. */

@@ -21,7 +21,7 @@
 // Compiled with -ffp-contract=off: every fp32 expression rounds exactly as
 // written, identical to the C oracle (oracle/icp_oracle.c) — XYZ, normals and
 // association indices are bit-exact given the same fp32 pose.  The
-// back-projection divides use a 3-instruction sequence only after
+// back-projection divides use a 2-instruction sequence only after
 // k_verify_fastdiv has proven it equal to IEEE division on the ENTIRE domain
 // those divides can see (d in [1, 32767], u in [0, W), v in [0, H)); otherwise
 // the IEEE path is compiled in.
@@ -38,6 +38,7 @@
 #include <string>
 #include <thread>
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <vector>
 
@@ -78,9 +79,14 @@ struct Intr {
     float fx, fy, cx, cy, ds;
 };
 
-// RN(1/fx), RN(1/fy), RN(1/ds) for the verified 3-op division.
+// Division by the constants fx, fy, ds in two operations (Brisebarre,
+// Muller & Raina, "Accelerating correctly rounded floating-point division
+// when the divisor is known in advance", IEEE TC 2004): for each divisor y,
+// h = RN(1/y) and l = RN((1 - y h) / y); then q = RN(n h + RN(n l)) =
+// fma(n, h, n * l).  Used only where k_verify_fastdiv finds it equal to IEEE
+// n / y on the whole domain the kernels divide.
 struct FastK {
-    float rfx, rfy, rds;
+    float hfx, lfx, hfy, lfy, hds, lds;
 };
 
 // 64-bit lane helpers (two 32-bit halves)
@@ -98,19 +104,17 @@ __device__ __forceinline__ double readlane64(double x, int l)
                   (unsigned)__builtin_amdgcn_readlane((int)hi32(x), l));
 }
 
-// q = RN(n * rd); r = n - q d (exact, fma); q + r rd (one rounding).
-// Equal to RN(n / d) wherever k_verify_fastdiv found no mismatch.
-__device__ __forceinline__ float div_fast(float n, float d, float rd)
+// fma(n, h, RN(n l)): equal to RN(n / d) wherever k_verify_fastdiv found
+// no mismatch (h, l of the divisor d, FastK).
+__device__ __forceinline__ float div_fast(float n, float h, float l)
 {
-    const float q = n * rd;
-    const float r = fmaf(-q, d, n);
-    return fmaf(r, rd, q);
+    return fmaf(n, h, n * l);
 }
 
 template <bool kFast>
-__device__ __forceinline__ float bp_div(float n, float d, float rd)
+__device__ __forceinline__ float bp_div(float n, float d, float h, float l)
 {
-    return kFast ? div_fast(n, d, rd) : n / d;
+    return kFast ? div_fast(n, h, l) : n / d;
 }
 
 // Spec a7's two projection quotients nu/den and nv/den, IEEE correctly
@@ -143,16 +147,16 @@ __device__ __forceinline__ bool proj_den_ok(float den)
     return (den >= 0x1p-60f) & (den <= 0x1p60f);
 }
 // Spec a7's projection reciprocal RN(1 / den): for den in [2^-60, 2^60] the
-// IEEE expansion of 1.0f / den rescales nothing (numerator 1, quotient in
-// [2^-60, 2^60]), so the chain reduces to the reciprocal refined by the two
-// correction steps of proj_div_one; youth_icp_selftest_projdiv compares it
-// with 1.0f / den for EVERY fp32 den in that range.  Outside: IEEE.
+// hardware reciprocal refined by ONE Newton step, fma(fma(-den, r0, 1), r0,
+// r0) (proj_recip), is already the correctly rounded 1.0f / den: measured
+// for EVERY fp32 den in that range (tools/rcp_probe.hip,
+// profiles/r02/rcp_probe.txt: 0 of 1,006,632,961 differ; the two further
+// quotient corrections used before changed nothing), and re-checked by
+// youth_icp_selftest_projdiv (tests/test_gpu_parity.py).  Outside: IEEE.
 __device__ __forceinline__ float proj_rcp_rn(float den)
 {
-    if (proj_den_ok(den)) {  // always in practice (den is a depth in metres)
-        const float r = proj_recip(den);
-        return proj_div_one(1.0f, den, r);
-    }
+    if (proj_den_ok(den))  // always in practice (den is a depth in metres)
+        return proj_recip(den);
     return 1.0f / den;
 }
 
@@ -196,9 +200,21 @@ template <bool kFast>
 __device__ __forceinline__ void backproject(int d, int u, int v, const Intr& K,
                                             const FastK& F, float& x, float& y, float& z)
 {
-    const float zz = bp_div<kFast>((float)max(d, 0), K.ds, F.rds);  // d <= 0: 0/ds = +0
-    x = bp_div<kFast>(((float)u - K.cx) * zz, K.fx, F.rfx);
-    y = bp_div<kFast>(((float)v - K.cy) * zz, K.fy, F.rfy);
+    const float zz = bp_div<kFast>((float)max(d, 0), K.ds, F.hds, F.lds);  // d <= 0: 0/ds = +0
+    x = bp_div<kFast>(((float)u - K.cx) * zz, K.fx, F.hfx, F.lfx);
+    y = bp_div<kFast>(((float)v - K.cy) * zz, K.fy, F.hfy, F.lfy);
+    z = zz;
+}
+// The same with the centred pixel coordinates uc = (float)u - cx and
+// vc = (float)v - cy supplied (exact: integers below 2^24), so a caller
+// walking a row forms them by additions.
+template <bool kFast>
+__device__ __forceinline__ void backproject_c(int d, float uc, float vc, const Intr& K,
+                                              const FastK& F, float& x, float& y, float& z)
+{
+    const float zz = bp_div<kFast>((float)max(d, 0), K.ds, F.hds, F.lds);
+    x = bp_div<kFast>(uc * zz, K.fx, F.hfx, F.lfx);
+    y = bp_div<kFast>(vc * zz, K.fy, F.hfy, F.lfy);
     z = zz;
 }
 
@@ -211,14 +227,14 @@ __global__ void k_verify_fastdiv(Intr K, FastK F, int W, int H, unsigned* bad)
     const int d = blockIdx.x * blockDim.x + threadIdx.x + 1;
     if (d > 32767) return;
     const float zi = (float)d / K.ds;
-    unsigned nb = (div_fast((float)d, K.ds, F.rds) != zi);
+    unsigned nb = (div_fast((float)d, F.hds, F.lds) != zi);
     for (int u = blockIdx.y; u < W; u += gridDim.y) {
         const float n = ((float)u - K.cx) * zi;
-        nb += (div_fast(n, K.fx, F.rfx) != n / K.fx);
+        nb += (div_fast(n, F.hfx, F.lfx) != n / K.fx);
     }
     for (int v = blockIdx.y; v < H; v += gridDim.y) {
         const float n = ((float)v - K.cy) * zi;
-        nb += (div_fast(n, K.fy, F.rfy) != n / K.fy);
+        nb += (div_fast(n, F.hfy, F.lfy) != n / K.fy);
     }
     if (nb) atomicAdd(bad, nb);
 }
@@ -930,8 +946,8 @@ __device__ __forceinline__ bool match_accumulate(float qx, float qy, float qz, f
                                                  const FastK& F, float thr2, double* acc)
 {
     const float tz = t.x;
-    const float tx = bp_div<kFast>((fu - K.cx) * tz, K.fx, F.rfx);
-    const float ty = bp_div<kFast>((fv - K.cy) * tz, K.fy, F.rfy);
+    const float tx = bp_div<kFast>((fu - K.cx) * tz, K.fx, F.hfx, F.lfx);
+    const float ty = bp_div<kFast>((fv - K.cy) * tz, K.fy, F.hfy, F.lfy);
     const float dx = qx - tx, dy = qy - ty, dz = qz - tz;
     const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
     const bool ok = in & (tz > 0.0f) & (d2 < thr2);
@@ -989,16 +1005,21 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
         float qx[4], qy[4], qz[4], fu[4], fv[4];
         bool in[4];
         int j[4];
+        // a lane's four pixels share one row when kAligned: centred
+        // coordinates by exact additions (uc0 + q == (float)(u0 + q) - cx)
+        const float uc0 = (float)u0 - K.cx, vc0 = (float)v0 - K.cy;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            int u = u0 + q, v = v0;
-            if (!kAligned) {
+            float sx, sy, sz;
+            if (kAligned) {
+                backproject_c<kFast>(dd[q], uc0 + (float)q, vc0, K, F, sx, sy, sz);
+            } else {
+                int u = u0 + q, v = v0;
                 const bool wrap = u >= W;
                 u = wrap ? u - W : u;
                 v = wrap ? v + 1 : v;
+                backproject<kFast>((i + q) < end ? dd[q] : 0, u, v, K, F, sx, sy, sz);
             }
-            float sx, sy, sz;
-            backproject<kFast>(kAligned || (i + q) < end ? dd[q] : 0, u, v, K, F, sx, sy, sz);
             xform_project(T, sx, sy, sz, K, W, H, qx[q], qy[q], qz[q], fu[q], fv[q], in[q], j[q]);
         }
         u0 += stepU;
@@ -1895,7 +1916,7 @@ struct youth_icp_ctx {
     int max_frames = 0;
     Intr K{};
     FastK F{};
-    bool fast = false;  // verified 3-op back-projection division
+    bool fast = false;  // verified 2-op back-projection division
     youth_icp_params prm{};
     hipStream_t stream = nullptr;
 
@@ -2393,6 +2414,22 @@ static int bind_device(youth_icp_ctx* c)
     return YOUTH_OK;
 }
 
+// FastK of the intrinsics: h = RN(1/y), l = RN((1 - y h) / y) with the
+// residual 1 - y h exact (fma) and the quotient rounded once from fp64 (any
+// l is safe: k_verify_fastdiv decides whether the pair is used).
+static FastK fast_consts(const youth_intrinsics& K)
+{
+    auto hl = [](float y, float& h, float& l) {
+        h = 1.0f / y;
+        l = (float)((double)std::fma(-y, h, 1.0f) / (double)y);
+    };
+    FastK F;
+    hl(K.fx, F.hfx, F.lfx);
+    hl(K.fy, F.hfy, F.lfy);
+    hl(K.depth_scale, F.hds, F.lds);
+    return F;
+}
+
 // Decide the division path for these intrinsics (k_verify_fastdiv).
 static int verify_fastdiv(youth_icp_ctx* c)
 {
@@ -2493,7 +2530,7 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
     c->max_frames = max_frames;
     const youth_intrinsics Kd = K ? *K : youth_default_intrinsics(W, H);
     c->K = Intr{Kd.fx, Kd.fy, Kd.cx, Kd.cy, Kd.depth_scale};
-    c->F = FastK{1.0f / Kd.fx, 1.0f / Kd.fy, 1.0f / Kd.depth_scale};
+    c->F = fast_consts(Kd);
     c->prm = P ? *P : youth_default_params();
     auto fail = [&](const char* what, hipError_t e) -> youth_icp_ctx* {
         set_error(YOUTH_EHIP, "youth_icp_create: %s (%d)", what, (int)e);
