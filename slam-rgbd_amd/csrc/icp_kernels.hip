@@ -1541,7 +1541,7 @@ constexpr int kCoopMaxPairs = 16;     // counter words per set: 16 x 8 x 32
 constexpr int kCoopErrWord = kCoopMaxPairs * kCoopShards * kCoopShardStride;
 constexpr int kCoopPrepWords = kCoopErrWord + kCoopShardStride;
 constexpr int kCoopSetWords = kCoopPrepWords + kCoopMaxPairs * kCoopShardStride;
-constexpr int kCoopTileH = 32;  // fused prep tiles: 64 x 32 pixels
+constexpr int kCoopTileH = 24;  // fused prep tiles: 64 x 24 pixels (one per workgroup of a 640x480 pair: 200 tiles, G = 200)
 constexpr unsigned kCoopSpinMax = 1u << 22;  // polls (~1 us each): seconds, never reached
 
 struct CoopState {
