@@ -177,7 +177,7 @@ void youth_icp_destroy(youth_icp_ctx* ctx);
 /* Device-resident align of n_pairs pairs.  d_src / d_dst: device pointers to
  * [n_pairs][H][W] int16 (d_src is read by every iteration: keep it alive and
  * unmodified until the align has completed on `stream`).  T_init: nullable HOST [n_pairs][16] fp64 (identity
- * if NULL).  d_T_out: nullable DEVICE [n_pairs][16] fp32.  stream: a
+ * if NULL; every entry must be finite, else YOUTH_EINVAL).  d_T_out: nullable DEVICE [n_pairs][16] fp32.  stream: a
  * hipStream_t as void* (NULL = the context's own stream).  Asynchronous:
  * returns after enqueueing; use youth_icp_sync / youth_icp_get_poses.  One
  * context's aligns must execute in order (one stream, or ordered by the
@@ -236,7 +236,7 @@ int youth_icp_get_plan(youth_icp_ctx* ctx, int* workgroups_per_pair, int* px_per
  * from v_rcp_f32 plus correction steps: *bit_mismatches counts bitwise
  * differences from IEEE 1.0f / den over EVERY fp32 den in the guarded range
  * [2^-60, 2^60] (must be 0); *proj_mismatches counts differences of the
- * projected pixel floor(fma(num, rz, c) + 0.5) or its in-range test against
+ * projected pixel floor(fma(num, rz, c + 0.5)) or its in-range test against
  * the IEEE reciprocal's on n pseudo-random (seeded) cases (must be 0). */
 int youth_icp_selftest_projdiv(int device, long long n, unsigned long long seed,
                                long long* bit_mismatches, long long* proj_mismatches);
@@ -276,7 +276,8 @@ int youth_icp_solve_host(youth_icp_ctx* ctx, const double* neq, double* T64);
 /* Upload one host depth frame into the context's 2-slot ring, back-project
  * it with normals and, when a reference frame is held, align it (source) to
  * the reference (target) with T_init (nullable host fp64 4x4; identity if
- * NULL).  The new frame then becomes the reference.  T_rel (host fp64 4x4):
+ * NULL; finite, else YOUTH_EINVAL and the frame is dropped).  The new frame
+ * then becomes the reference.  T_rel (host fp64 4x4):
  * P_ref = T_rel * P_new, identity for the first frame (*has_ref = 0).
  * Returns status bits (>= 0) or a negative YOUTH_E* code.  Synchronous. */
 int youth_icp_track_frame(youth_icp_ctx* ctx, const int16_t* depth,

@@ -91,10 +91,11 @@ static inline int assoc_one(float sx, float sy, float sz, const float T[12],
     const float qy = fmaf(T[6], sz, fmaf(T[5], sy, fmaf(T[4], sx, T[7])));
     const float qz = fmaf(T[10], sz, fmaf(T[9], sy, fmaf(T[8], sx, T[11])));
     if (!(qz > 0.0f)) return -1;
-    /* one correctly rounded reciprocal, then fx P'x rz + cx in one rounding */
+    /* one correctly rounded reciprocal, then fx P'x rz + (cx + 0.5) in one
+     * rounding (cx + 0.5 is exact: cx is a pixel coordinate) */
     const float rz = 1.0f / qz;
-    const float fu = floorf(fmaf(K->fx * qx, rz, K->cx) + 0.5f);
-    const float fv = floorf(fmaf(K->fy * qy, rz, K->cy) + 0.5f);
+    const float fu = floorf(fmaf(K->fx * qx, rz, K->cx + 0.5f));
+    const float fv = floorf(fmaf(K->fy * qy, rz, K->cy + 0.5f));
     if (!(fu >= 0.0f && fu < (float)W && fv >= 0.0f && fv < (float)H)) return -1;
     const int j = (int)fv * W + (int)fu;
     const float tz = tZ[j];

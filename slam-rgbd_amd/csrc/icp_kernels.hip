@@ -242,7 +242,7 @@ __global__ void k_verify_fastdiv(Intr K, FastK F, int W, int H, unsigned* bad)
 // Self-test of the projection reciprocal (proj_rcp_rn) against IEEE 1.0f / den:
 // bad[0]: bitwise mismatches over EVERY fp32 den in [2^-60, 2^60] (the
 //         guarded range: exhaustive, ~1.0e9 values; must be 0);
-// bad[1]: mismatches of the projected pixel floor(fma(num, rz, c) + 0.5) and
+// bad[1]: mismatches of the projected pixel floor(fma(num, rz, c + 0.5)) and
 //         its in-range test [0, 65536) between proj_rcp_rn and 1.0f / den on
 //         `n` SplitMix64 cases (den any positive finite fp32 incl. outside the
 //         guard, num random with exponent in [-80, 80] or next to a
@@ -281,8 +281,8 @@ __global__ void k_selftest_projdiv(unsigned long long n, unsigned long long seed
                                   (unsigned)((r3 >> 63) << 31));
         }
         const float c = (float)(r2 >> 52);  // [0, 4096)
-        const float ui = floorf(fmaf(num, 1.0f / den, c) + 0.5f);
-        const float uf = floorf(fmaf(num, proj_rcp_rn(den), c) + 0.5f);
+        const float ui = floorf(fmaf(num, 1.0f / den, c + 0.5f));
+        const float uf = floorf(fmaf(num, proj_rcp_rn(den), c + 0.5f));
         const bool ii = (ui >= 0.0f) & (ui < 65536.0f), inf_ = (uf >= 0.0f) & (uf < 65536.0f);
         if (ii != inf_ || (ii && ui != uf)) ++b1;
     }
@@ -909,7 +909,7 @@ struct PoseState {
 // with the same roundings (fmaf = one rounding, -ffp-contract=off elsewhere).
 //   a7  P' = R P + t:  P'_i = fma(R_i2, z, fma(R_i1, y, fma(R_i0, x, t_i)))
 //       valid iff z > 0 and P'_z > 0;  rz = RN(1 / P'_z);
-//       u' = floor(fma(fx P'_x, rz, cx) + 0.5), v' likewise; in range of the
+//       u' = floor(fma(fx P'_x, rz, cx + 0.5)), v' likewise; in range of the
 //       target frame.  Unmatched pixels compute on safe values (branch-free)
 //       and gather record 0.
 __device__ __forceinline__ void xform_project(const float* T, float sx, float sy, float sz,
@@ -921,14 +921,19 @@ __device__ __forceinline__ void xform_project(const float* T, float sx, float sy
     qz = fmaf(T[10], sz, fmaf(T[9], sy, fmaf(T[8], sx, T[11])));
     const bool vz = (sz > 0.0f) & (qz > 0.0f);
     const float rz = proj_rcp_rn(vz ? qz : 1.0f);
-    const float uu = floorf(fmaf(K.fx * qx, rz, K.cx) + 0.5f);
-    const float vv = floorf(fmaf(K.fy * qy, rz, K.cy) + 0.5f);
-    in = vz & (uu >= 0.0f) & (uu < (float)W) & (vv >= 0.0f) & (vv < (float)H);
+    const float uu = floorf(fmaf(K.fx * qx, rz, K.cx + 0.5f));
+    const float vv = floorf(fmaf(K.fy * qy, rz, K.cy + 0.5f));
+    // 0 <= u' < W and 0 <= v' < H on the integer values: uu, vv are finite
+    // integral floats (T finite, youth_icp.h), v_cvt_i32_f32 saturates
+    // outside the int range, and a negative one wraps to >= 2^31 unsigned,
+    // so the unsigned compares equal the spec's four float compares
+    const int iu = (int)uu, iv = (int)vv;
+    in = vz & ((unsigned)iu < (unsigned)W) & ((unsigned)iv < (unsigned)H);
     fu = in ? uu : 0.0f;
     fv = in ? vv : 0.0f;
-    // 0 when !in; v', W <= 16384 (youth_icp_create): the 24-bit multiply is
-    // exact and full rate
-    j = (int)__umul24((unsigned)(int)fv, (unsigned)W) + (int)fu;
+    // 0 when !in; v', W <= 16384 (youth_icp_create): the 24-bit multiply-add
+    // is exact and full rate
+    j = in ? (int)__umul24((unsigned)iv, (unsigned)W) + iu : 0;
 }
 
 //   a7  gate: target valid with a normal (k_prep stores z = 0 for a target
@@ -2314,6 +2319,12 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
     if (rc) return rc;
     const double* dTi = nullptr;
     if (T_init_host) {
+        // finite initial poses keep every projected coordinate finite, which
+        // the kernels' integer in-range test relies on (xform_project)
+        for (size_t i = 0; i < (size_t)n_pairs * 16; ++i)
+            if (!std::isfinite(T_init_host[i]))
+                return set_error(YOUTH_EINVAL, "T_init: non-finite entry in pair %d",
+                                 (int)(i / 16));
         HIP_TRY(hipMemcpyAsync(c->d_Tinit, T_init_host, (size_t)n_pairs * 16 * sizeof(double),
                                hipMemcpyHostToDevice, s));
         dTi = c->d_Tinit;

@@ -598,6 +598,29 @@ def test_kernel_paths_skipped_update(monkeypatch, mode):
         assert np.array_equal(Tdev[p], T32[p])
 
 
+def test_non_finite_T_init_rejected():
+    """T_init must be finite (the kernels' integer in-range test relies on
+    finite projected coordinates): a NaN or inf entry is YOUTH_EINVAL before
+    anything is enqueued, and the context keeps working."""
+    import torch
+    src, dst, _ = youth_synth.pairs(60, 2, 160, 120)
+    ds, dd = torch.from_numpy(src).cuda(), torch.from_numpy(dst).cuda()
+    torch.cuda.synchronize()
+    with youth_icp.IcpContext(160, 120, 2) as ctx:
+        for bad in (np.nan, np.inf):
+            T_init = np.tile(np.eye(4), (2, 1, 1))
+            T_init[1, 0, 3] = bad
+            with pytest.raises(youth_icp.IcpError) as e:
+                ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), 2, T_init=T_init)
+            assert e.value.code == youth_icp.YOUTH_EINVAL
+        ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), 2)
+        ctx.sync()
+        T64, _, st = ctx.get_poses(2)
+    for p in range(2):
+        To, _, sto, _ = oracle.align(src[p], dst[p])
+        assert st[p] == sto and _pose_err(T64[p], To) <= POSE_TOL
+
+
 def test_max_frame_size_8192x8192():
     """The largest frame youth_icp_create accepts (W*H = 2^26): 24-bit index
     multiply, 32-bit record byte offsets and the persistent path (one pair is
