@@ -22,7 +22,7 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -T --output-format c
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --kernel-trace -T --output-format csv -d $OUT/pmc_sq -o pmc \
     -- python3 bench.py $ARGS > $OUT/bench_sq.log 2>&1
 python3 tools/pmc_summary.py $OUT > $OUT/pmc_summary.txt
-python3 tools/pmc_traffic.py $OUT $OUT/traffic.json 512 640 480 10 > /dev/null
+python3 tools/pmc_traffic.py $OUT $OUT/traffic.json ${PAIRS:-512} 640 480 10 > /dev/null
 KT=$(find $OUT/kt -name '*kernel_trace.csv' -print -quit)
 python3 tools/kt_summary.py $KT 5 > $OUT/kt_summary.txt
 cp "$(find $OUT/kt -name '*kernel_stats.csv' -print -quit)" $OUT/kernel_stats.csv
