@@ -54,7 +54,7 @@ namespace {
 // clamped fetch or a float4 load past N reads an invalid point (z = 0).
 // Sources are read straight from the caller's int16 depth.
 constexpr int kTileW = 64;
-constexpr int kTileH = 16;
+constexpr int kTileH = 24;  // k_prep tiles 64 x 24 (16: 651 us, 24: 629 us, 32: 739 us per 512 frames; profiles/r02/ab_s13_prep_tiles.txt)
 constexpr int kPrepThreads = 256;
 constexpr int kLdsW = kTileW + 2;
 constexpr int kLdsH = kTileH + 2;
