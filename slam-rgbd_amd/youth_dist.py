@@ -12,6 +12,8 @@ Pure torch.distributed; no device code here.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -119,3 +121,95 @@ def compose_trajectory(rel: np.ndarray) -> np.ndarray:
     for k in range(rel.shape[0]):
         out[k + 1] = out[k] @ rel[k]
     return out
+
+
+# ---- the C-ABI RCCL gather (include/youth_dist.h, libyouth_dist.so) --------
+# For one-process-per-GPU hosts that do not use torch.distributed: the same
+# contiguous shards, one ncclAllGather of the padded largest shard and a
+# compaction kernel.  Python binding for the tests (tests/test_gpu_bench.py).
+DIST_ID_BYTES = 128
+_dist_lib = None
+
+
+def _dist():
+    global _dist_lib
+    if _dist_lib is None:
+        import ctypes
+        from ctypes import POINTER, c_char_p, c_int, c_void_p
+        import youth_icp
+        youth_icp.load_library()  # libyouth_icp.so first (DT_NEEDED of libyouth_dist.so)
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libyouth_dist.so")
+        if not os.path.exists(path):
+            raise OSError(f"{path} not built: run `make -C {os.path.dirname(path)}`")
+        lib = ctypes.CDLL(path)
+        sig = {
+            "youth_dist_unique_id": (c_int, [c_char_p]),
+            "youth_dist_create": (c_void_p, [c_int, c_int, c_int, c_char_p]),
+            "youth_dist_allgather_poses": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+            "youth_dist_allgather_poses_host": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
+            "youth_dist_row_source": (c_int, [c_int, c_int, c_int, POINTER(c_int), POINTER(c_int)]),
+            "youth_dist_nranks": (c_int, [c_void_p]),
+            "youth_dist_rank": (c_int, [c_void_p]),
+            "youth_dist_destroy": (None, [c_void_p]),
+            "youth_dist_last_error": (c_char_p, []),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _dist_lib = lib
+    return _dist_lib
+
+
+def _dist_check(rc):
+    import youth_icp
+    if rc < 0:
+        raise youth_icp.IcpError(rc, (_dist().youth_dist_last_error() or b"").decode())
+
+
+def row_source(n_pairs, nranks, row):
+    """youth_dist_row_source -> (rank, index in its shard)."""
+    import ctypes
+    q, i = ctypes.c_int(0), ctypes.c_int(0)
+    _dist_check(_dist().youth_dist_row_source(n_pairs, nranks, row, ctypes.byref(q),
+                                               ctypes.byref(i)))
+    return q.value, i.value
+
+
+def unique_id() -> bytes:
+    import ctypes
+    buf = ctypes.create_string_buffer(DIST_ID_BYTES)
+    _dist_check(_dist().youth_dist_unique_id(buf))
+    return buf.raw
+
+
+class RcclPoseGather:
+    """youth_dist_create / allgather_poses(_host) / destroy."""
+
+    def __init__(self, nranks: int, rank: int, device: int, uid: bytes):
+        import youth_icp
+        lib = _dist()
+        self._h = lib.youth_dist_create(nranks, rank, device, uid)
+        if not self._h:
+            msg = (lib.youth_dist_last_error() or b"").decode()
+            code = youth_icp.YOUTH_ENODEV if "no HIP device" in msg else youth_icp.YOUTH_EHIP
+            raise youth_icp.IcpError(code, msg)
+
+    def allgather_device(self, d_local: int, n_pairs: int, d_all: int, stream: int = 0):
+        _dist_check(_dist().youth_dist_allgather_poses(self._h, d_local or None, n_pairs, d_all,
+                                                       stream or None))
+
+    def allgather_host(self, local, n_pairs: int):
+        import numpy as np
+        loc = np.ascontiguousarray(local, np.float32).reshape(-1, 16)
+        out = np.zeros((n_pairs, 16), np.float32)
+        _dist_check(_dist().youth_dist_allgather_poses_host(
+            self._h, loc.ctypes.data if loc.size else None, n_pairs, out.ctypes.data))
+        return out
+
+    def close(self):
+        if self._h:
+            _dist().youth_dist_destroy(self._h)
+            self._h = None
+
+    __del__ = close

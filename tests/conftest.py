@@ -29,7 +29,8 @@ def pytest_configure(config):
 
 def _ensure_built():
     need = [os.path.join(PKG, "libyouth_icp.so"), os.path.join(PKG, "libyouth_synth.so"),
-            os.path.join(PKG, "slam_host_demo"), os.path.join(PKG, "batch_multi_demo")]
+            os.path.join(PKG, "slam_host_demo"), os.path.join(PKG, "batch_multi_demo"), os.path.join(PKG, "batch_rccl_demo"),
+            os.path.join(PKG, "libyouth_dist.so")]
     if not all(os.path.exists(p) for p in need):
         subprocess.run(["make", "-C", PKG, "-j8"], check=True, stdout=subprocess.DEVNULL)
     if not os.path.exists(os.path.join(ORACLE, "liboracle.so")):

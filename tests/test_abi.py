@@ -18,6 +18,7 @@ HEADERS = {
     "youth_wire.h": os.path.join(PKG, "libyouth_icp.so"),
     "youth_viewer.h": os.path.join(PKG, "libyouth_icp.so"),
     "youth_synth.h": os.path.join(PKG, "libyouth_synth.so"),
+    "youth_dist.h": os.path.join(PKG, "libyouth_dist.so"),
 }
 
 
@@ -111,6 +112,24 @@ def test_shard_range_matches_bench_split():
         youth_icp.shard_range(8, 0, 0)
     with pytest.raises(youth_icp.IcpError):
         youth_icp.shard_range(8, 2, 2)
+
+
+def test_rccl_gather_row_mapping_and_no_device(has_gpu):
+    """youth_dist.h (libyouth_dist.so, the multi-process RCCL pose gather):
+    the row -> (rank, row-in-shard) mapping its compaction kernel applies
+    inverts youth_icp_shard_range for every split; without a device the
+    communicator is refused loudly."""
+    import youth_dist
+    for n in (1, 5, 8, 63, 64, 512, 999):
+        for k in (1, 2, 3, 4, 7, 8):
+            for r in range(n):
+                q, i = youth_dist.row_source(n, k, r)
+                f, c = youth_icp.shard_range(n, k, q)
+                assert f + i == r and 0 <= i < c
+    if not has_gpu:
+        with pytest.raises(youth_icp.IcpError) as e:
+            youth_dist.RcclPoseGather(1, 0, 0, bytes(youth_dist.DIST_ID_BYTES))
+        assert e.value.code == youth_icp.YOUTH_ENODEV
 
 
 def test_queue_overflow_policy_matches_reference():

@@ -654,3 +654,44 @@ def test_plain_c_batch_multi_demo(tmp_path):
     assert not st.any()
     for p in range(n):
         assert _pose_err(T[p], T_cpu[p]) <= POSE_TOL, p
+
+
+def test_rccl_pose_gather_c_abi_one_rank():
+    """youth_dist.h through RCCL on this box's GPU at N = 1 (the
+    multi-process form needs one GPU per rank; N > 1 is the driver's 8-GPU
+    run): the device and host gathers return every row in pair order."""
+    import torch
+    import youth_dist
+    g = youth_dist.RcclPoseGather(1, 0, 0, youth_dist.unique_id())
+    try:
+        rng = np.random.default_rng(5)
+        for n in (1, 37, 512):
+            loc = rng.standard_normal((n, 16)).astype(np.float32)
+            assert np.array_equal(g.allgather_host(loc, n), loc)
+            d_loc = torch.from_numpy(loc).cuda()
+            d_all = torch.zeros_like(d_loc)
+            s = torch.cuda.current_stream()
+            g.allgather_device(d_loc.data_ptr(), n, d_all.data_ptr(), s.cuda_stream)
+            torch.cuda.synchronize()
+            assert torch.equal(d_all, d_loc)
+    finally:
+        g.close()
+
+
+def test_plain_c_rccl_demo_one_rank(tmp_path):
+    """examples/batch_rccl_demo.c (one process per GPU: shard align +
+    youth_dist_allgather_poses_host) as rank 0 of 1: id file bootstrap, the
+    gathered poses within 1e-5 of the oracle."""
+    import subprocess
+    from conftest import PKG
+    n, W, H = 4, 320, 240
+    out = str(tmp_path / "T.f32")
+    r = subprocess.run([os.path.join(PKG, "batch_rccl_demo"), "1", "0", str(tmp_path / "id"),
+                        str(n), out, str(W), str(H)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    T = np.fromfile(out, np.float32).reshape(n, 4, 4)
+    src, dst, _ = youth_synth.pairs(0, n, W, H)
+    T_cpu, st = oracle.align_batch(src, dst, iters=10, n_threads=min(n, os.cpu_count() or 1))
+    assert not st.any()
+    for p in range(n):
+        assert _pose_err(T[p], T_cpu[p]) <= POSE_TOL, p
