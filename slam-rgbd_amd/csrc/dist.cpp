@@ -124,7 +124,9 @@ int youth_dist_allgather_poses(youth_dist* d, const float* d_local, int n_pairs,
     const hipStream_t s = (hipStream_t)stream;
     const size_t rows = (size_t)d->nranks * max_count;
     if (rows > d->scratch_rows) {
-        if (d->scratch && hipFree(d->scratch) != hipSuccess) return fail(YOUTH_EHIP, "hipFree");
+        // a previous gather may still read the old scratch on some stream
+        if (d->scratch && (hipDeviceSynchronize() != hipSuccess || hipFree(d->scratch) != hipSuccess))
+            return fail(YOUTH_EHIP, "hipFree scratch");
         d->scratch = nullptr;
         d->scratch_rows = 0;
         if (hipMalloc(&d->scratch, rows * 16 * sizeof(float)) != hipSuccess)
@@ -160,7 +162,9 @@ int youth_dist_allgather_poses_host(youth_dist* d, const float* h_local, int n_p
         return fail(YOUTH_EHIP, "hipStreamCreate");
     const size_t rows = (size_t)count + n_pairs;
     if (rows > d->staging_rows) {
-        if (d->staging && hipFree(d->staging) != hipSuccess) return fail(YOUTH_EHIP, "hipFree");
+        if (d->staging && (hipStreamSynchronize(d->stream) != hipSuccess ||
+                           hipFree(d->staging) != hipSuccess))
+            return fail(YOUTH_EHIP, "hipFree staging");
         d->staging = nullptr;
         d->staging_rows = 0;
         if (hipMalloc(&d->staging, rows * 16 * sizeof(float)) != hipSuccess)
