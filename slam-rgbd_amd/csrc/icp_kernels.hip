@@ -1981,14 +1981,17 @@ struct youth_icp_ctx {
 
 static int reduce_geometry(const youth_icp_ctx* c, int n_pairs, int* chunk_out)
 {
-    // ~3072 work chunks per iteration (persistent kernel at 64 pairs: best of
-    // 1536..4096; fewer chunks make items wait for their pair's pose, more
-    // pay the per-item hand-off: DESIGN.md §5), at least 8 pixels per lane.
-    static const int target_blocks = [] {
+    // work chunks per iteration: fewer chunks make items wait for their
+    // pair's pose, more pay the per-item hand-off.  Measured
+    // best (tools/chunk_sweep.sh, profiles/r02/chunk_sweep.txt): ~2048 up to
+    // 256 pairs per launch (64 pairs: +2.4 %, 128: +3.4 % over 3072), ~3072
+    // above.  At least 8 pixels per lane.
+    static const int knob = [] {
         const char* e = getenv("YOUTH_ICP_TARGET_CHUNKS");  // tuning knob
         const int v = e ? atoi(e) : 0;
-        return v > 0 ? v : 3072;
+        return v > 0 ? v : 0;
     }();
+    const int target_blocks = knob ? knob : (n_pairs <= 256 ? 2048 : 3072);
     int nb = (target_blocks + n_pairs - 1) / n_pairs;
     const int max_nb = (c->N + 2 * kRedStep - 1) / (2 * kRedStep);
     if (nb > max_nb) nb = max_nb;
