@@ -30,6 +30,7 @@ Rank 0 prints ONE JSON line.
 import argparse
 import hashlib
 import json
+import math
 import os
 import sys
 import time
@@ -70,6 +71,10 @@ def parse():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--min-warmup-ms", type=float, default=50.0,
+                    help="after the --warmup steps, run more untimed steps until the warm-up has "
+                         "lasted this long (the GPU's clock ramps over ~10-20 ms from idle; "
+                         "reported as warmup_steps_run); 0 = exactly --warmup steps")
     ap.add_argument("--windows", type=int, default=3,
                     help="extra timed windows of --steps steps after the timed region (spread)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -140,8 +145,23 @@ class Run:
         `windows` more K-step windows (spread) and a short pass timing every
         kernel kind (k_prep)."""
         a = self.a
+        t0 = time.perf_counter()
         for _ in range(a.warmup):
             step()
+        self.warmup_steps_run = a.warmup
+        if a.warmup > 0 and a.min_warmup_ms > 0:
+            # W steps of a small shard (64 pairs: 5 x 0.9 ms) end before the
+            # clock has ramped up: the first timed window then ran 11 % below
+            # the steady windows (profiles/r02/warm_probe.txt).  Same count on
+            # every rank: a step holds the RCCL gather.
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            need = a.min_warmup_ms * 1e-3 - el
+            extra = min(100000, math.ceil(need / (el / a.warmup))) if need > 0 else 0
+            extra = int(self.max_over_ranks(float(extra)))
+            for _ in range(extra):
+                step()
+            self.warmup_steps_run += extra
         ctx.set_timing(True, iteration_kernel_only=True)
         elapsed = self.window(step, a.steps)
         kt = {"k_icp": ctx.get_timing(0)}
@@ -591,6 +611,8 @@ def base_result(R, value, elapsed):
         "n_gpus": R.world,
         "steps": a.steps,
         "warmup": a.warmup,
+        "warmup_steps_run": getattr(R, "warmup_steps_run", a.warmup),
+        "min_warmup_ms": a.min_warmup_ms,
         "ms_per_step": elapsed / a.steps * 1e3,
         "higher_is_better": True,
         "scaling": "strong",
