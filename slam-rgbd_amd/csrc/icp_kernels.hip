@@ -658,32 +658,33 @@ __device__ __forceinline__ int solve_update_wave(const double* neq, double* T64,
     }
     if (!(maxd > 0.0)) return YOUTH_STATUS_DEGENERATE;
     const double eps = 1e-12 * maxd;
-    double Ar[6], Lr[6], D[6], Dinv[6];
+    // LDL^T right-looking: lane i holds row i, S[j] = A[i][j] minus the
+    // terms of the columns done so far.  Every element receives the same
+    // subtractions in the same order (m increasing) as the left-looking
+    // spec (solve6), so the results are bit-identical; but column m's
+    // updates of the later columns and its forward-substitution step are
+    // independent of column m+1's pivot divide and overlap it.  No early
+    // exit inside the loop (one basic block): a failed pivot is flagged and
+    // returned after it (nothing is stored before).
+    double S[6], Lr[6], D[6], Dinv[6];
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
-        Ar[j] = neq[i <= j ? tri6(i, j) : tri6(j, i)];
-        Lr[j] = 0.0;
-    }
-    // LDL^T, column j: lane i computes A[i][j] - sum_m (L[i][m] L[j][m]) D[m]
-    // (lane j: the pivot d_j); L[i][j] = s / d_j below the diagonal
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-        double sj = Ar[j];
-#pragma unroll
-        for (int m = 0; m < j; ++m) sj -= (Lr[m] * readlane64(Lr[m], j)) * D[m];
-        const double d = readlane64(sj, j);
-        if (!(d > eps)) return YOUTH_STATUS_DEGENERATE;
-        D[j] = d;
-        Dinv[j] = 1.0 / d;  // one divide per pivot; every use multiplies
-        Lr[j] = lane > j ? sj * Dinv[j] : (lane == j ? 1.0 : 0.0);
-    }
-    // forward: y_i = (-b_i - sum_{m<i} L[i][m] y_m) / d_i
+    for (int j = 0; j < 6; ++j) S[j] = neq[i <= j ? tri6(i, j) : tri6(j, i)];
+    // forward: y_i = (-b_i - sum_{m<i} L[i][m] y_m) / d_i, step m right after column m
     double y = -neq[21 + i];
+    bool bad = false;
 #pragma unroll
     for (int m = 0; m < 6; ++m) {
+        const double d = readlane64(S[m], m);
+        bad |= !(d > eps);
+        D[m] = d;
+        Dinv[m] = 1.0 / d;  // one divide per pivot; every use multiplies
+        Lr[m] = lane > m ? S[m] * Dinv[m] : (lane == m ? 1.0 : 0.0);
+#pragma unroll
+        for (int j = m + 1; j < 6; ++j) S[j] -= (Lr[m] * readlane64(Lr[m], j)) * D[m];
         const double ym = readlane64(y, m);
         y = lane > m ? y - Lr[m] * ym : y;
     }
+    if (bad) return YOUTH_STATUS_DEGENERATE;
     double dinv = Dinv[0];
 #pragma unroll
     for (int j = 1; j < 6; ++j) dinv = i == j ? Dinv[j] : dinv;
