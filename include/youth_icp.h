@@ -253,8 +253,9 @@ int youth_icp_selftest_normalize(int device, long long n, unsigned long long see
 /* --- Stage-level entry points (validation / parity tests) --------------- */
 
 /* Depth -> XYZ planes (+ normals when want_normals) for n_frames host frames.
- * Outputs are HOST arrays [n_frames][H*W] each (any may be NULL).  Same
- * kernel as the align path. */
+ * Outputs are HOST arrays [n_frames][H*W] each (any may be NULL).  With X, Y
+ * and Z all NULL the records come from the align path's record kernel (no
+ * planes stored), else from the same kernel storing the planes too. */
 int youth_icp_prepare_host(youth_icp_ctx* ctx, const int16_t* depth,
                            int n_frames, int want_normals, float* X, float* Y,
                            float* Z, float* NX, float* NY, float* NZ);

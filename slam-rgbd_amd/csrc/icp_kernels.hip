@@ -2845,7 +2845,8 @@ int youth_icp_prepare_host(youth_icp_ctx* c, const int16_t* depth, int n_frames,
     const size_t N = c->N;
     HIP_TRY(hipMemcpyAsync(c->d_depth, depth, (size_t)n_frames * N * sizeof(int16_t),
                            hipMemcpyHostToDevice, s));
-    rc = launch_prep(c, s, c->d_depth, n_frames, 0, true);
+    // no X/Y/Z wanted: the align path's record kernel (k_prep without planes)
+    rc = launch_prep(c, s, c->d_depth, n_frames, 0, X || Y || Z);
     if (rc) return rc;
     float* outs[6] = {X, Y, Z, NX, NY, NZ};
     for (int f = 0; f < n_frames; ++f)

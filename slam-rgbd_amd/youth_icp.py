@@ -384,13 +384,17 @@ class IcpContext:
         return {"kernel": "k_prep + k_icp (persistent)"}
 
     # host-array stage entry points (parity tests)
-    def prepare(self, depth: np.ndarray, want_normals: bool = True):
+    def prepare(self, depth: np.ndarray, want_normals: bool = True, want_xyz: bool = True):
+        """Stage a2/a6 on host frames: X, Y, Z planes and the record normals
+        (NX, NY, NZ).  want_xyz=False asks for the normals only, which runs the
+        align path's record kernel exactly as an align does (no X/Y/Z planes
+        stored; X/Y/Z come back as zeros)."""
         d = np.ascontiguousarray(depth, np.int16).reshape(-1, self.H, self.W)
         n = d.shape[0]
         outs = [np.zeros((n, self.H, self.W), np.float32) for _ in range(6)]
+        ptrs = [_p(o, c_float) if (k >= 3 or want_xyz) else None for k, o in enumerate(outs)]
         _check(self._lib.youth_icp_prepare_host(self._ctx, _p(d, c_int16), n,
-                                                1 if want_normals else 0,
-                                                *[_p(o, c_float) for o in outs]))
+                                                1 if want_normals else 0, *ptrs))
         return outs
 
     def reduce(self, src: np.ndarray, dst: np.ndarray, T12: np.ndarray, want_assoc=True):

@@ -71,6 +71,24 @@ def test_prepare_bit_exact(W, H):
             assert np.array_equal(_bits(g), _bits(o)), f
 
 
+@pytest.mark.parametrize("W,H,n", [(640, 480, 12), (1280, 960, 3), (96, 64, 40), (97, 53, 3)])
+def test_prepare_records_align_path_bit_exact(W, H, n):
+    """The align path's record kernel as an align runs it (no X/Y/Z planes;
+    wide and narrow halo loads, many tiles) gives the oracle's normals bit for
+    bit, and the same as the stage-level call that also stores the planes."""
+    src, dst, _ = youth_synth.pairs(21, (n + 1) // 2, W, H)
+    frames = np.concatenate([src, dst])[:n]
+    frames[0, 1, :5] = [-1, -32768, 32767, 0, 1]
+    with youth_icp.IcpContext(W, H, n) as ctx:
+        rec = ctx.prepare(frames, want_normals=True, want_xyz=False)
+        ref = ctx.prepare(frames, want_normals=True, want_xyz=True)
+    for f in range(n):
+        oN = oracle.normals(*oracle.backproject(frames[f]))
+        for g, r, o in zip(rec[3:], ref[3:], oN):
+            assert np.array_equal(_bits(g[f]), _bits(o)), f
+            assert np.array_equal(_bits(g[f]), _bits(r[f])), f
+
+
 @pytest.mark.parametrize("name", ["pair_80x60", "pair_160x120", "pair_97x53"])
 def test_prepare_matches_golden(name):
     g = _load(name)
