@@ -468,28 +468,49 @@ def c5_rate(R, F=1000, sample_every=16, stream_frames=300, reps=3):
 
 def streamed_rate(a, frames, rel_batch):
     """The sequence streamed frame by frame from HOST memory through the
-    tracker (youth_icp_track_frame: processSlamFrame's path): per frame one
-    614 KB H2D, target prep of the new frame + 10 iterations against the
-    previous one (one k_icp_coop launch), pose D2H, synchronous.  Relative
-    poses checked against the batch run's (fp32 output rounding)."""
+    tracker (processSlamFrame's worker path): per frame one 614 KB copy into
+    pinned staging + H2D on a transfer stream, target prep of the new frame +
+    10 iterations against the previous one (one k_icp_coop launch), pose D2H.
+    `value`: pipelined two deep as the SLAM worker runs it
+    (youth_icp_track_submit / _collect: frame k+1's copy and H2D overlap frame
+    k's align); `sync_value`: youth_icp_track_frame, one frame at a time.
+    Relative poses checked against the batch run's (fp32 output rounding) and
+    the two modes against each other (bitwise)."""
     n = frames.shape[0]
     ctx = youth_icp.IcpContext(a.width, a.height, 2, iters=a.iters)
     ctx.track_frame(frames[0])
     ctx.track_frame(frames[1])                         # warm
     ctx.track_reset()
     t0 = time.perf_counter()
-    rel = []
+    sync = []
     for f in range(n):
         T, st, has = ctx.track_frame(frames[f])
+        if has:
+            sync.append(T)
+    el_sync = time.perf_counter() - t0
+    ctx.track_reset()
+    t0 = time.perf_counter()
+    rel = []
+    for f in range(n):
+        ctx.track_submit(frames[f])
+        if ctx.track_pending() == 2:
+            T, st, has = ctx.track_collect()
+            if has:
+                rel.append(T)
+    while ctx.track_pending():
+        T, st, has = ctx.track_collect()
         if has:
             rel.append(T)
     el = time.perf_counter() - t0
     plan = ctx.get_plan()
     ctx.close()
     return {"frames": n, "value": n / el, "unit": "frames/s", "us_per_frame": el / n * 1e6,
+            "sync_value": n / el_sync, "sync_us_per_frame": el_sync / n * 1e6,
             "kernel_path": plan,
             "max_abs_diff_vs_batch_poses": pose_err(np.stack(rel), rel_batch[: n - 1]),
-            "note": "host frames, H2D + align + pose D2H per frame, synchronous"}
+            "pipelined_equals_sync": bool(np.array_equal(np.stack(rel), np.stack(sync))),
+            "note": "host frames, copy to pinned + H2D + align + pose D2H per frame; value: two "
+                    "frames in flight (track_submit/collect), sync_value: track_frame"}
 
 
 def survey_noise_parity(a, ctx, main, n=16):

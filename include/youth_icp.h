@@ -284,6 +284,22 @@ int youth_icp_solve_host(youth_icp_ctx* ctx, const double* neq, double* T64);
 int youth_icp_track_frame(youth_icp_ctx* ctx, const int16_t* depth,
                           const double* T_init, double* T_rel, int* has_ref);
 
+/* Pipelined form of youth_icp_track_frame (the SLAM API's worker uses it):
+ * youth_icp_track_submit copies the host frame into a pinned staging buffer
+ * (the caller's buffer is free on return), enqueues its H2D on a transfer
+ * stream and its align (against the frame submitted before it) on the
+ * context's stream, and returns without waiting, so the next frame's copy
+ * overlaps this frame's align.  At most 2 frames may be in flight
+ * (YOUTH_EINVAL otherwise).  youth_icp_track_collect waits for the OLDEST
+ * submitted frame and returns exactly what youth_icp_track_frame would have
+ * returned for it (status bits or a negative code, T_rel, *has_ref).
+ * youth_icp_track_frame = submit + collect, with nothing in flight. */
+int youth_icp_track_submit(youth_icp_ctx* ctx, const int16_t* depth,
+                           const double* T_init);
+int youth_icp_track_collect(youth_icp_ctx* ctx, double* T_rel, int* has_ref);
+/* Frames submitted and not yet collected (0, 1 or 2). */
+int youth_icp_track_pending(const youth_icp_ctx* ctx);
+
 /* Forget the reference frame (next tracked frame starts a new sequence). */
 void youth_icp_track_reset(youth_icp_ctx* ctx);
 

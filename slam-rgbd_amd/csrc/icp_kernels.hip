@@ -1567,6 +1567,9 @@ struct CoopState {
     // they are for a later launch (the tracker's next reference frame)
     const int16_t* prep_src;
     int prep_out0, prep_wait, prep_wide;
+    // pair 0's result straight into pinned host memory (the tracker): fp64
+    // 4x4 pose [16], then the status word; null: none
+    double* res_host;
 };
 
 // Phase timestamps for tools/coopbench only (never in the product build):
@@ -1861,7 +1864,12 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
         cs.T64[(size_t)p * 16 + i] = v;
         if (i < 12) cs.T32[(size_t)p * 12 + i] = (float)v;
         if (cs.T_out) cs.T_out[(size_t)p * 16 + i] = i < 12 ? (float)v : (i == 15 ? 1.0f : 0.0f);
-        if (i == 0) cs.status[p] = st_acc | (timeout ? YOUTH_STATUS_TIMEOUT : 0);
+        const int32_t st = st_acc | (timeout ? YOUTH_STATUS_TIMEOUT : 0);
+        if (i == 0) cs.status[p] = st;
+        if (cs.res_host && p == 0) {
+            cs.res_host[i] = v;
+            if (i == 0) reinterpret_cast<int32_t*>(cs.res_host + 16)[0] = st;
+        }
     }
 }
 
@@ -1967,6 +1975,18 @@ struct youth_icp_ctx {
     hipStream_t last_stream = nullptr;
 
     int track_ref = -1;  // ring slot (0/1) of the tracker's reference frame
+    double* coop_res_host = nullptr;  // set around a tracker align: k_icp_coop writes its result there
+    // pipelined tracking (youth_icp_track_submit / _collect): up to two frames
+    // in flight, each with a pinned staging buffer, pinned results and events
+    struct TrackSlot {
+        int16_t* pinned = nullptr;     // host depth copy, H2D source
+        double* res = nullptr;         // pinned: T64 [16], then the status word
+        hipEvent_t h2d = nullptr;      // staging -> device depth done (xfer)
+        hipEvent_t done = nullptr;     // align + result D2H done (stream)
+        int has_ref = 0;
+    } trk[2];
+    hipEvent_t trk_depth_free[2] = {nullptr, nullptr};  // last align reading depth slot d
+    int trk_head = 0, trk_n = 0;       // oldest in-flight submission, count in flight
 
     // host-buffer batch API: H2D of chunk k+1 on xfer overlaps the align of chunk k
     hipStream_t xfer = nullptr;
@@ -2284,7 +2304,8 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
     CoopState cs{dTi,      c->d_T64, c->d_T32, c->d_status,          c->d_stats,
                  d_T_out,  set,      set_next, c->d_head,            iters,
                  n_pairs,  G,        npx,      job ? job->depth : nullptr,
-                 job ? job->out0 : 0, job && job->wait ? 1 : 0, wide ? 1 : 0};
+                 job ? job->out0 : 0, job && job->wait ? 1 : 0, wide ? 1 : 0,
+                 c->coop_res_host};
     const float4* recs = c->d_rec;
     size_t P = c->P;
     int W = c->W, H = c->H;
@@ -2507,6 +2528,14 @@ void youth_icp_destroy(youth_icp_ctx* c)
         }
     if (c->xfer) (void)hipStreamSynchronize(c->xfer);
     for (hipEvent_t e : c->xfer_ev) (void)hipEventDestroy(e);
+    for (auto& q : c->trk) {
+        if (q.pinned) (void)hipHostFree(q.pinned);
+        if (q.res) (void)hipHostFree(q.res);
+        if (q.h2d) (void)hipEventDestroy(q.h2d);
+        if (q.done) (void)hipEventDestroy(q.done);
+    }
+    for (hipEvent_t e : c->trk_depth_free)
+        if (e) (void)hipEventDestroy(e);
     void* bufs[] = {c->d_depth, c->d_rec,   c->d_xyz,      c->d_T64, c->d_T32,   c->d_status,
                     c->d_Tinit, c->d_stats, c->d_partials, c->d_neq, c->d_assoc, c->d_Tout,
                     c->d_flag,  c->d_arrivals, c->d_arr_it, c->d_epoch, c->d_head,
@@ -3119,45 +3148,126 @@ int youth_icp_align_batch_multi(const int16_t* src, const int16_t* dst, int n_pa
 }
 
 // ------------------------------------------------------ frame tracking --
+// Lazily: the transfer stream, two pinned staging/result slots and events.
+static int ensure_track(youth_icp_ctx* c)
+{
+    if (c->trk[1].done) return YOUTH_OK;
+    if (!c->xfer) HIP_TRY(hipStreamCreateWithFlags(&c->xfer, hipStreamNonBlocking));
+    for (auto& q : c->trk) {
+        if (!q.pinned)
+            HIP_TRY(hipHostMalloc((void**)&q.pinned, (size_t)c->N * sizeof(int16_t),
+                                  hipHostMallocDefault));
+        if (!q.res) HIP_TRY(hipHostMalloc((void**)&q.res, 17 * sizeof(double), hipHostMallocDefault));
+        if (!q.h2d) HIP_TRY(hipEventCreateWithFlags(&q.h2d, hipEventDisableTiming));
+    }
+    for (auto& e : c->trk_depth_free)
+        if (!e) {
+            HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            HIP_TRY(hipEventRecord(e, c->stream));
+        }
+    for (auto& q : c->trk)
+        if (!q.done) HIP_TRY(hipEventCreateWithFlags(&q.done, hipEventDisableTiming));
+    return YOUTH_OK;
+}
+
+int youth_icp_track_submit(youth_icp_ctx* c, const int16_t* depth, const double* T_init)
+{
+    if (!c || !depth) return set_error(YOUTH_EINVAL, "track_submit: bad arguments");
+    if (c->trk_n >= 2)
+        return set_error(YOUTH_EINVAL, "track_submit: two frames in flight (collect one first)");
+    if (T_init)
+        for (int i = 0; i < 16; ++i)
+            if (!std::isfinite(T_init[i]))
+                return set_error(YOUTH_EINVAL, "T_init: non-finite entry in pair 0");
+    int rc = bind_device(c);
+    if (rc) return rc;
+    rc = ensure_track(c);
+    if (rc) return rc;
+    hipStream_t s = c->stream;
+    const size_t N = c->N;
+    auto& q = c->trk[(c->trk_head + c->trk_n) & 1];
+    // the new frame goes to the ring slot that is not the reference; its depth
+    // was last read (as a source) by the align two submissions back
+    const int slot = c->track_ref == 0 ? 1 : 0;
+    memcpy(q.pinned, depth, N * sizeof(int16_t));  // the caller's buffer is free on return
+    HIP_TRY(hipStreamWaitEvent(c->xfer, c->trk_depth_free[slot], 0));
+    HIP_TRY(hipMemcpyAsync(c->d_depth + (size_t)slot * N, q.pinned, N * sizeof(int16_t),
+                           hipMemcpyHostToDevice, c->xfer));
+    HIP_TRY(hipEventRecord(q.h2d, c->xfer));
+    HIP_TRY(hipStreamWaitEvent(s, q.h2d, 0));
+    // the new frame is the next submission's target: its records go to `slot`
+    // (beside this call's iterations, which gather ref's records)
+    const PrepJob job{c->d_depth + (size_t)slot * N, 1, slot, false};
+    const int ref = c->track_ref;
+    q.has_ref = ref >= 0;
+    if (ref < 0) {
+        rc = launch_prep(c, s, job.depth, 1, slot, false);
+    } else {
+        // source: the new frame's depth; target: ref's records.  k_icp_coop
+        // writes the result into the pinned slot itself (no copies on the
+        // stream); any other kernel path copies it
+        c->coop_res_host = q.res;
+        rc = run_iterations(c, s, c->d_depth + (size_t)slot * N, PairMap{0, ref}, 1, T_init,
+                            nullptr, nullptr, &job);
+        c->coop_res_host = nullptr;
+        if (rc == YOUTH_OK && !c->last_coop) {
+            HIP_TRY(hipMemcpyAsync(q.res, c->d_T64, 16 * sizeof(double), hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipMemcpyAsync(q.res + 16, c->d_status, sizeof(int32_t),
+                                   hipMemcpyDeviceToHost, s));
+        }
+    }
+    if (rc) {
+        // nothing of this frame is kept; wait for what was enqueued so the
+        // staging buffer and the ring slot are not in use by a dropped frame
+        (void)hipStreamSynchronize(s);
+        (void)hipStreamSynchronize(c->xfer);
+        return rc;
+    }
+    HIP_TRY(hipEventRecord(c->trk_depth_free[slot], s));
+    HIP_TRY(hipEventRecord(q.done, s));
+    c->track_ref = slot;
+    ++c->trk_n;
+    return YOUTH_OK;
+}
+
+int youth_icp_track_collect(youth_icp_ctx* c, double* T_rel, int* has_ref)
+{
+    if (!c || !T_rel) return set_error(YOUTH_EINVAL, "track_collect: bad arguments");
+    if (c->trk_n == 0) return set_error(YOUTH_EINVAL, "track_collect: no frame in flight");
+    int rc = bind_device(c);
+    if (rc) return rc;
+    auto& q = c->trk[c->trk_head];
+    c->trk_head ^= 1;
+    --c->trk_n;
+    HIP_TRY(hipEventSynchronize(q.done));
+    if (has_ref) *has_ref = q.has_ref;
+    if (!q.has_ref) {
+        for (int i = 0; i < 16; ++i) T_rel[i] = (i % 5) == 0 ? 1.0 : 0.0;
+        return 0;
+    }
+    for (int i = 0; i < 12; ++i) T_rel[i] = q.res[i];
+    T_rel[12] = 0.0;
+    T_rel[13] = 0.0;
+    T_rel[14] = 0.0;
+    T_rel[15] = 1.0;
+    int32_t st;
+    memcpy(&st, q.res + 16, sizeof(st));
+    return st;
+}
+
+int youth_icp_track_pending(const youth_icp_ctx* c)
+{
+    return c ? c->trk_n : 0;
+}
+
 int youth_icp_track_frame(youth_icp_ctx* c, const int16_t* depth, const double* T_init,
                           double* T_rel, int* has_ref)
 {
     if (!c || !depth || !T_rel) return set_error(YOUTH_EINVAL, "track_frame: bad arguments");
-    int rc = bind_device(c);
+    if (c->trk_n) return set_error(YOUTH_EINVAL, "track_frame: submitted frames not collected");
+    const int rc = youth_icp_track_submit(c, depth, T_init);
     if (rc) return rc;
-    hipStream_t s = c->stream;
-    const size_t N = c->N;
-    const int slot = c->track_ref == 0 ? 1 : 0;
-    HIP_TRY(hipMemcpyAsync(c->d_depth + (size_t)slot * N, depth, N * sizeof(int16_t),
-                           hipMemcpyHostToDevice, s));
-    // the new frame is the next call's target: its records go to `slot`
-    // (beside this call's iterations, which gather ref's records)
-    const PrepJob job{c->d_depth + (size_t)slot * N, 1, slot, false};
-    int32_t st = 0;
-    const int ref = c->track_ref;
-    if (has_ref) *has_ref = ref >= 0;
-    if (ref < 0) {
-        rc = launch_prep(c, s, job.depth, 1, slot, false);
-        if (rc) return rc;
-    } else {
-        // source: the new frame's depth (staging slot); target: ref's records
-        rc = run_iterations(c, s, c->d_depth + (size_t)slot * N, PairMap{0, ref}, 1, T_init,
-                            nullptr, nullptr, &job);
-        if (rc) return rc;
-        HIP_TRY(hipMemcpyAsync(T_rel, c->d_T64, 16 * sizeof(double), hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(&st, c->d_status, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    }
-    HIP_TRY(hipStreamSynchronize(s));
-    if (ref < 0) {
-        for (int i = 0; i < 16; ++i) T_rel[i] = (i % 5) == 0 ? 1.0 : 0.0;
-    } else {
-        T_rel[12] = 0.0;
-        T_rel[13] = 0.0;
-        T_rel[14] = 0.0;
-        T_rel[15] = 1.0;
-    }
-    c->track_ref = slot;
-    return st;
+    return youth_icp_track_collect(c, T_rel, has_ref);
 }
 
 void youth_icp_track_reset(youth_icp_ctx* c)

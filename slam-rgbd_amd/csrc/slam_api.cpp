@@ -4,7 +4,8 @@
 // Same entry points, argument meaning, 1/0 return convention and threading
 // model (caller threads enqueue; ONE private worker thread tracks), but the
 // ORB-SLAM3 TrackRGBD call (SLAM.cpp:54) is replaced by HIP frame-to-frame
-// point-to-plane ICP (youth_icp_track_frame).  Host-only C++: no HIP types.
+// point-to-plane ICP (youth_icp_track_submit / _collect, two frames in
+// flight).  Host-only C++: no HIP types.
 //
 // Differences from the reference that are deliberate:
 //  - processSlamFrame keeps depth as int16 millimetres (the GPU converts with
@@ -193,6 +194,11 @@ youth_intrinsics intrinsics_for(int w, int h)
 }
 
 // SLAM.cpp:32-63 processFramesThread, with TrackRGBD replaced by HIP ICP.
+// Pipelined two deep (youth_icp_track_submit / _collect): after submitting
+// frame k the worker collects frame k-1, so frame k's upload and align run
+// while the host records k-1's pose and pops k+1.  A frame's pose reaches
+// the trajectory when the next frame is submitted or the queue runs empty
+// (the worker stays busy until then: youth_slam_wait_idle).
 void worker_main(int device)
 {
     fprintf(stderr, "youth_icp: SLAM processing thread started\n");
@@ -200,6 +206,40 @@ void worker_main(int device)
     int cw = 0, ch = 0;
     std::vector<int16_t> buf;
     double T_w_ref[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    struct Pending {
+        uint32_t ts;
+        int npts;
+    };
+    std::deque<Pending> pend;  // submitted, not yet collected (oldest first)
+    // collect the oldest submitted frame; record its pose unless a reset
+    // arrived since it was submitted
+    auto finish_one = [&](bool record) {
+        const Pending pr0 = pend.front();
+        pend.pop_front();
+        double T_rel[16];
+        int has_ref = 0;
+        const int st = youth_icp_track_collect(ctx, T_rel, &has_ref);
+        if (st < 0) {
+            fprintf(stderr, "youth_icp: tracking failed: %s\n", youth_icp_last_error());
+            return;
+        }
+        if (!record || g_reset.load()) return;
+        std::lock_guard<std::mutex> lk(g_slam_mu);
+        if (!has_ref || g_traj.empty()) {
+            // new sequence: this frame is the world origin
+            double I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+            memcpy(T_w_ref, I, sizeof(I));
+            g_traj.clear();
+        } else {
+            // P_ref = T_rel P_new  =>  T_w_new = T_w_ref * T_rel
+            mat_mul4(T_w_ref, T_rel, T_w_ref);
+        }
+        PoseRec pr;
+        pr.ts = pr0.ts;
+        memcpy(pr.T, T_w_ref, sizeof(pr.T));
+        g_traj.push_back(pr);
+        g_last_points = pr0.npts;
+    };
     while (g_process.load()) {
         if (buf.empty()) buf.resize((size_t)4096 * 4096);
         int w = 0, h = 0;
@@ -207,12 +247,20 @@ void worker_main(int device)
         g_busy.store(true);
         const int got = youth_queue_pop(g_queue, buf.data(), buf.size(), &w, &h, &ts);
         if (got != 1) {
+            if (!pend.empty()) {  // nothing new: finish what is in flight
+                finish_one(true);
+                continue;
+            }
             g_busy.store(false);
             std::this_thread::sleep_for(std::chrono::milliseconds(got == 0 ? 1 : 5));
             continue;
         }
-        if (g_reset.exchange(false) && ctx) youth_icp_track_reset(ctx);
+        if (g_reset.exchange(false)) {
+            while (!pend.empty()) finish_one(false);  // frames of the old sequence
+            if (ctx) youth_icp_track_reset(ctx);
+        }
         if (!ctx || w != cw || h != ch) {
+            while (!pend.empty()) finish_one(true);
             if (ctx) youth_icp_destroy(ctx);
             const youth_intrinsics K = intrinsics_for(w, h);
             ctx = youth_icp_create(device, w, h, 2, &K, nullptr);
@@ -226,35 +274,16 @@ void worker_main(int device)
                 continue;
             }
         }
-        double T_rel[16];
-        int has_ref = 0;
-        const int st = youth_icp_track_frame(ctx, buf.data(), nullptr, T_rel, &has_ref);
-        if (st < 0) {
-            fprintf(stderr, "youth_icp: tracking failed: %s\n", youth_icp_last_error());
-            g_busy.store(false);
-            continue;
-        }
         int npts = 0;
         for (size_t i = 0; i < (size_t)w * h; ++i) npts += buf[i] > 0;
-        {
-            std::lock_guard<std::mutex> lk(g_slam_mu);
-            if (!has_ref || g_traj.empty()) {
-                // new sequence: this frame is the world origin
-                double I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
-                memcpy(T_w_ref, I, sizeof(I));
-                g_traj.clear();
-            } else {
-                // P_ref = T_rel P_new  =>  T_w_new = T_w_ref * T_rel
-                mat_mul4(T_w_ref, T_rel, T_w_ref);
-            }
-            PoseRec pr;
-            pr.ts = ts;
-            memcpy(pr.T, T_w_ref, sizeof(pr.T));
-            g_traj.push_back(pr);
-            g_last_points = npts;
+        if (youth_icp_track_submit(ctx, buf.data(), nullptr) < 0) {
+            fprintf(stderr, "youth_icp: tracking failed: %s\n", youth_icp_last_error());
+            continue;
         }
-        g_busy.store(false);
+        pend.push_back(Pending{ts, npts});
+        if (pend.size() == 2) finish_one(true);
     }
+    while (ctx && !pend.empty()) finish_one(true);
     if (ctx) youth_icp_destroy(ctx);
     fprintf(stderr, "youth_icp: SLAM processing thread stopped\n");
 }

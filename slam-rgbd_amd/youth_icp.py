@@ -116,6 +116,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "youth_icp_solve_host": (c_int, [c_void_p, PD, PD]),
         "youth_icp_track_frame": (c_int, [c_void_p, P16, PD, PD, POINTER(c_int)]),
         "youth_icp_track_reset": (None, [c_void_p]),
+        "youth_icp_track_submit": (c_int, [c_void_p, P16, PD]),
+        "youth_icp_track_collect": (c_int, [c_void_p, PD, POINTER(c_int)]),
+        "youth_icp_track_pending": (c_int, [c_void_p]),
         "youth_parse_camera_yaml": (c_int, [c_char_p, POINTER(Intrinsics), POINTER(c_int),
                                             POINTER(c_int)]),
         "youth_queue_create": (c_void_p, [c_int, c_int]),
@@ -426,6 +429,24 @@ class IcpContext:
 
     def track_reset(self) -> None:
         self._lib.youth_icp_track_reset(self._ctx)
+
+    def track_submit(self, depth: np.ndarray, T_init=None) -> None:
+        """Pipelined tracking: enqueue one host frame (copied before the call
+        returns) and return without waiting; at most 2 in flight."""
+        d = np.ascontiguousarray(depth, np.int16)
+        Ti = None if T_init is None else np.ascontiguousarray(T_init, np.float64)
+        _check(self._lib.youth_icp_track_submit(self._ctx, _p(d, c_int16), _p(Ti, c_double)))
+
+    def track_collect(self):
+        """(T_rel, status, has_ref) of the OLDEST submitted frame (waits for it)."""
+        T = np.zeros((4, 4), np.float64)
+        has = c_int(0)
+        st = _check(self._lib.youth_icp_track_collect(self._ctx, _p(T, c_double),
+                                                      ctypes.byref(has)))
+        return T, st, bool(has.value)
+
+    def track_pending(self) -> int:
+        return int(self._lib.youth_icp_track_pending(self._ctx))
 
 
 def selftest_projdiv(n: int, seed: int = 1, device: int = 0) -> tuple[int, int]:

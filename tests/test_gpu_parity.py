@@ -391,6 +391,46 @@ def test_track_frame_matches_oracle():
         assert not has
 
 
+def test_track_submit_collect_pipelined():
+    """Two frames in flight (the SLAM worker's pattern): every collected
+    result equals the synchronous track_frame sequence bit for bit, in any
+    submit/collect interleaving; a reset with frames in flight starts a new
+    sequence at the next submission; misuse is refused (EINVAL)."""
+    frames, _ = youth_synth.sequence(3, 9)
+    with youth_icp.IcpContext(640, 480, 2) as ref:
+        want = [ref.track_frame(f) for f in frames]
+    with youth_icp.IcpContext(640, 480, 2) as ctx:
+        with pytest.raises(youth_icp.IcpError):
+            ctx.track_collect()                              # nothing in flight
+        got = []
+        order = "SCSSCCSSCSCSCSCSCC"   # S = submit next frame, C = collect oldest (<= 2 in flight)
+        k = 0
+        for op in order:
+            if op == "S":
+                ctx.track_submit(frames[k])
+                k += 1
+            else:
+                got.append(ctx.track_collect())
+        assert k == len(frames) and len(got) == len(frames) and ctx.track_pending() == 0
+        for (Tg, sg, hg), (Tw, sw, hw) in zip(got, want):
+            assert np.array_equal(Tg, Tw) and sg == sw and hg == hw
+        ctx.track_submit(frames[0])
+        ctx.track_submit(frames[1])
+        with pytest.raises(youth_icp.IcpError):
+            ctx.track_submit(frames[2])                      # a third frame in flight
+        with pytest.raises(youth_icp.IcpError):
+            ctx.track_frame(frames[2])                       # frames not collected
+        ctx.track_reset()                                    # frames 0 and 1 in flight
+        _, _, h0 = ctx.track_collect()
+        ctx.track_submit(frames[2])
+        _, _, h1 = ctx.track_collect()
+        _, _, h2 = ctx.track_collect()
+        assert h0 and h1 and not h2                          # frame 2 starts a new sequence
+        T, st, has = ctx.track_frame(frames[3])
+        T64, _, sto, _ = oracle.align(frames[3], frames[2])
+        assert has and st == sto and _pose_err(T, T64) <= POSE_TOL
+
+
 # ------------------------------------------------------- SLAM.h drop-in --
 def test_slam_api_end_to_end():
     frames, Twc = youth_synth.sequence(0, 8)

@@ -1,8 +1,9 @@
 /*
- * icp_stub.c — TEST INFRASTRUCTURE ONLY: a CPU stand-in for the six
+ * icp_stub.c — TEST INFRASTRUCTURE ONLY: a CPU stand-in for the
  * libyouth_icp device entry points the host-side threading code calls
- * (slam_api.cpp's worker: create / destroy / track_frame / track_reset /
- * device_count / last_error, plus youth_default_intrinsics), so the SLAM.h
+ * (slam_api.cpp's worker: create / destroy / track_submit / track_collect /
+ * track_frame / track_reset / device_count / last_error, plus
+ * youth_default_intrinsics), so the SLAM.h
  * queue + worker, the AlgorithmModule frame loop and the POSIX-queue
  * transport can run under ThreadSanitizer / AddressSanitizer on a machine
  * without a GPU (SURVEY §5 "Race detection").  It is linked only into the
@@ -20,6 +21,9 @@
 struct youth_icp_ctx {
     int W, H, has_ref;
     long long ref_sum;
+    /* submitted frames' results, oldest first (at most 2) */
+    double T[2][16];
+    int has[2], n, head;
 };
 
 int youth_icp_device_count(void) { return 1; }
@@ -43,14 +47,45 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
 void youth_icp_destroy(youth_icp_ctx* c) { free(c); }
 void youth_icp_track_reset(youth_icp_ctx* c) { c->has_ref = 0; }
 
+static int stub_track(youth_icp_ctx* c, const int16_t* depth, double* T_rel, int* has_ref);
+
+int youth_icp_track_submit(youth_icp_ctx* c, const int16_t* depth, const double* T_init)
+{
+    (void)T_init;
+    if (c->n >= 2) return YOUTH_EINVAL;
+    const int j = (c->head + c->n) & 1;
+    stub_track(c, depth, c->T[j], &c->has[j]);
+    ++c->n;
+    return 0;
+}
+
+int youth_icp_track_collect(youth_icp_ctx* c, double* T_rel, int* has_ref)
+{
+    if (c->n == 0) return YOUTH_EINVAL;
+    struct timespec ts = {0, 200 * 1000}; /* a GPU align takes ~100 us */
+    nanosleep(&ts, NULL);
+    memcpy(T_rel, c->T[c->head], 16 * sizeof(double));
+    if (has_ref) *has_ref = c->has[c->head];
+    c->head ^= 1;
+    --c->n;
+    return 0;
+}
+
+int youth_icp_track_pending(const youth_icp_ctx* c) { return c->n; }
+
 int youth_icp_track_frame(youth_icp_ctx* c, const int16_t* depth, const double* T_init,
                           double* T_rel, int* has_ref)
 {
     (void)T_init;
+    struct timespec ts = {0, 200 * 1000};
+    nanosleep(&ts, NULL);
+    return stub_track(c, depth, T_rel, has_ref);
+}
+
+static int stub_track(youth_icp_ctx* c, const int16_t* depth, double* T_rel, int* has_ref)
+{
     long long s = 0;
     for (int i = 0; i < c->W * c->H; ++i) s += depth[i];
-    struct timespec ts = {0, 200 * 1000};  /* a GPU align takes ~100 us */
-    nanosleep(&ts, NULL);
     memset(T_rel, 0, 16 * sizeof(double));
     T_rel[0] = T_rel[5] = T_rel[10] = T_rel[15] = 1.0;
     if (has_ref) *has_ref = c->has_ref;
