@@ -461,7 +461,10 @@ __device__ __forceinline__ void prep_tile(const int16_t* __restrict__ dep, float
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, rec), rrec,
                                                    (int)(i * sizeof(float4)), 0, 16);
         } else {
-            R[i] = rec;
+            // non-temporal: k_prep's 16 B/px stream of records is read back
+            // by k_icp only after the whole batch is written (610 vs 626 us
+            // per 512 frames, profiles/r02/ab_s30.txt, ab_s31.txt)
+            __builtin_nontemporal_store(__builtin_bit_cast(u4v, rec), reinterpret_cast<u4v*>(R) + i);
         }
     }
 }

@@ -246,7 +246,11 @@ __global__ __launch_bounds__(kCloudThreads) void k_cloud_emit(
     for (int g = threadIdx.x; g * 4 < end; g += kCloudThreads) {
         const int j = g * 4;
         if (j >= head && j + 4 <= end) {
-            *reinterpret_cast<float4*>(base + j) = *reinterpret_cast<const float4*>(stage + j);
+            // non-temporal: the list is for the renderer, not re-read here
+            // (111 vs 121 us per 64-frame call, profiles/r02/ab_s31.txt)
+            typedef float f4nt __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store(*reinterpret_cast<const f4nt*>(stage + j),
+                                        reinterpret_cast<f4nt*>(base + j));
         } else {
 #pragma unroll
             for (int q = 0; q < 4; ++q)

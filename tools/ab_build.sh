@@ -15,6 +15,9 @@ cd $ROOT/slam-rgbd_amd
 make -s build/slam_api.o build/algorithm_module.o build/wire.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize \
     ${HIPFLAGS_EXTRA:-} -I../include -Icsrc -c $OUT/icp_kernels.hip -o $OUT/icp_kernels.o
+# the viewer kernels: the tree's, or env VIEWER_SRC (a viewer_cloud.hip variant)
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize \
+    -I../include -Icsrc -c ${VIEWER_SRC:-csrc/viewer_cloud.hip} -o $OUT/viewer_cloud.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libyouth_icp.so $OUT/icp_kernels.o \
-    build/slam_api.o build/algorithm_module.o build/wire.o -lpthread -lrt -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
+    $OUT/viewer_cloud.o build/slam_api.o build/algorithm_module.o build/wire.o -lpthread -lrt -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
 echo "$OUT/libyouth_icp.so"

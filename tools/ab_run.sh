@@ -19,7 +19,7 @@ for r in $(seq 1 $R); do
     python3 - "$label" "$r" <<'PY'
 import json,sys
 d=json.loads(open(f"gpurun_out/ab/{sys.argv[1]}.{sys.argv[2]}.json").read().strip().splitlines()[-1])
-print(f"{sys.argv[1]:>10s} round {sys.argv[2]}: {d['value']:9.0f} aligns/s  kernel {d['roofline']['avg_launch_ms']*1e3:7.1f} us  prep {d['kernel_ms_per_step']['k_prep']*1e3:6.1f} us  err {d.get('parity',{}).get('pose_max_abs_err_vs_cpu',float('nan')):.1e}  sched {d.get('sched_last_step')}", flush=True)
+print(f"{sys.argv[1]:>10s} round {sys.argv[2]}: {d['value']:9.0f} aligns/s  kernel {d['roofline']['avg_launch_ms']*1e3:7.1f} us  prep {d['kernel_ms_per_step']['k_prep']*1e3:6.1f} us  err {d.get('parity',{}).get('pose_max_abs_err_vs_cpu',float('nan')):.1e}  sched {d.get('sched_last_step')}" + (f"  viewer {d['viewer_cloud']['us_per_call']:.1f} us" if 'viewer_cloud' in d else ""), flush=True)
 PY
   done
 done
