@@ -401,9 +401,11 @@ class IcpContext:
         return outs
 
     def reduce(self, src: np.ndarray, dst: np.ndarray, T12: np.ndarray, want_assoc=True):
-        s = np.ascontiguousarray(src, np.int16)
-        d = np.ascontiguousarray(dst, np.int16)
+        s, _ = self._frame_args(src, None)
+        d, _ = self._frame_args(dst, None)
         T = np.ascontiguousarray(np.asarray(T12, np.float32).reshape(-1)[:12])
+        if T.size != 12:
+            raise ValueError("T12 must hold 12 values (3x4)")
         assoc = np.zeros(self.W * self.H, np.int32) if want_assoc else None
         neq = np.zeros(YOUTH_NEQ, np.float64)
         _check(self._lib.youth_icp_reduce_host(self._ctx, _p(s, c_int16), _p(d, c_int16),
@@ -418,9 +420,17 @@ class IcpContext:
                                                    _p(T, c_double)))
         return T, st
 
-    def track_frame(self, depth: np.ndarray, T_init=None):
+    def _frame_args(self, depth, T_init):
         d = np.ascontiguousarray(depth, np.int16)
+        if d.size != self.W * self.H:
+            raise ValueError(f"depth frame of {d.size} pixels; the context is {self.W}x{self.H}")
         Ti = None if T_init is None else np.ascontiguousarray(T_init, np.float64)
+        if Ti is not None and Ti.size != 16:
+            raise ValueError("T_init must be a 4x4 matrix")
+        return d, Ti
+
+    def track_frame(self, depth: np.ndarray, T_init=None):
+        d, Ti = self._frame_args(depth, T_init)
         T = np.zeros((4, 4), np.float64)
         has = c_int(0)
         st = _check(self._lib.youth_icp_track_frame(self._ctx, _p(d, c_int16), _p(Ti, c_double),
@@ -433,8 +443,7 @@ class IcpContext:
     def track_submit(self, depth: np.ndarray, T_init=None) -> None:
         """Pipelined tracking: enqueue one host frame (copied before the call
         returns) and return without waiting; at most 2 in flight."""
-        d = np.ascontiguousarray(depth, np.int16)
-        Ti = None if T_init is None else np.ascontiguousarray(T_init, np.float64)
+        d, Ti = self._frame_args(depth, T_init)
         _check(self._lib.youth_icp_track_submit(self._ctx, _p(d, c_int16), _p(Ti, c_double)))
 
     def track_collect(self):
@@ -475,6 +484,8 @@ def align_batch(src: np.ndarray, dst: np.ndarray, K: Intrinsics | None = None, i
     d = np.ascontiguousarray(dst, np.int16)
     if s.ndim == 2:
         s, d = s[None], d[None]
+    if s.ndim != 3 or s.shape != d.shape:
+        raise ValueError(f"src {s.shape} and dst {d.shape} must both be [n, H, W]")
     n, H, W = s.shape
     T = np.zeros((n, 4, 4), np.float32)
     assoc = np.zeros((n, H * W), np.int32) if want_assoc else None
@@ -494,6 +505,8 @@ def align_batch_multi(src: np.ndarray, dst: np.ndarray, K: Intrinsics | None = N
     d = np.ascontiguousarray(dst, np.int16)
     if s.ndim == 2:
         s, d = s[None], d[None]
+    if s.ndim != 3 or s.shape != d.shape:
+        raise ValueError(f"src {s.shape} and dst {d.shape} must both be [n, H, W]")
     n, H, W = s.shape
     T = np.zeros((n, 4, 4), np.float32)
     st = np.zeros(n, np.int32)

@@ -189,3 +189,16 @@ def test_synth_sequence_shards_consistent():
     full, T = youth_synth.sequence(0, 6, 64, 48)
     part, T2 = youth_synth.sequence(3, 3, 64, 48)
     assert np.array_equal(full[3:], part) and np.array_equal(T[3:], T2)
+
+
+def test_host_wrappers_reject_mismatched_shapes():
+    """Shape checks run before any library call (no GPU needed): a frame stack
+    whose src and dst differ, or that is not [n, H, W], is a ValueError, not an
+    out-of-bounds read in the library."""
+    a = np.zeros((2, 8, 8), np.int16)
+    with pytest.raises(ValueError):
+        youth_icp.align_batch(a, np.zeros((2, 8, 9), np.int16))
+    with pytest.raises(ValueError):
+        youth_icp.align_batch_multi(a, np.zeros((3, 8, 8), np.int16))
+    with pytest.raises(ValueError):
+        youth_icp.align_batch(np.zeros(64, np.int16), np.zeros(64, np.int16))
