@@ -1573,6 +1573,10 @@ struct CoopState {
     // pair 0's result straight into pinned host memory (the tracker): fp64
     // 4x4 pose [16], then the status word; null: none
     double* res_host;
+    // 1: workgroup c's source pixels are target tile c (kTileW x kCoopTileH,
+    // = npx x kThreads pixels), the tile it preps, so its iteration-0 gathers
+    // (small motion) hit records it has just written; 0: a contiguous run
+    int tile_src;
 };
 
 // Phase timestamps for tools/coopbench only (never in the product build):
@@ -1719,13 +1723,26 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
     {
         const int16_t* sD = dsrc + (size_t)(pm.src0 + p) * N;
         const int base = c * npx * kThreads + threadIdx.x;
+        const int tiles_x = (W + kTileW - 1) / kTileW;
+        const int tyc = c / tiles_x;
+        const int tx0 = (c - tyc * tiles_x) * kTileW, ty0 = tyc * kCoopTileH;
         for (int s = 0; s < npx; ++s) {
-            const int i = base + s * kThreads;
-            const int d = i < N ? (int)sD[i] : 0;
-            const int ii = i < N ? i : 0;
-            const int v = ii / W;
+            int u, v;
+            bool inr;
+            if (cs.tile_src) {
+                const int k = s * kThreads + threadIdx.x;
+                u = tx0 + (k & (kTileW - 1));
+                v = ty0 + k / kTileW;
+                inr = u < W && v < H;
+            } else {
+                const int i = base + s * kThreads;
+                inr = i < N;
+                v = inr ? i / W : 0;
+                u = inr ? i - v * W : 0;
+            }
+            const int d = inr ? (int)sD[(size_t)v * W + u] : 0;
             float x, y, z;
-            backproject<kFast>(d, ii - v * W, v, K, F, x, y, z);
+            backproject<kFast>(d, inr ? u : 0, inr ? v : 0, K, F, x, y, z);
             X[s * kThreads + threadIdx.x] = x;
             Y[s * kThreads + threadIdx.x] = y;
             Z[s * kThreads + threadIdx.x] = z;
@@ -1979,6 +1996,7 @@ struct youth_icp_ctx {
 
     int track_ref = -1;  // ring slot (0/1) of the tracker's reference frame
     double* coop_res_host = nullptr;  // set around a tracker align: k_icp_coop writes its result there
+    bool coop_tile_src = true;        // YOUTH_ICP_COOP_TILE_SRC=0: contiguous source chunks
     // pipelined tracking (youth_icp_track_submit / _collect): up to two frames
     // in flight, each with a pinned staging buffer, pinned results and events
     struct TrackSlot {
@@ -2304,11 +2322,16 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
     unsigned* set_next = c->d_coop + (size_t)(c->coop_par ^ 1) * kCoopSetWords;
     c->coop_par ^= 1;
     const bool wide = job && (c->W % 4 == 0) && (reinterpret_cast<uintptr_t>(job->depth) % 8 == 0);
+    // tile-shaped source chunks when one target tile is exactly one
+    // workgroup's pixels and the pair has one workgroup per tile
+    const int tiles = ((c->W + kTileW - 1) / kTileW) * ((c->H + kCoopTileH - 1) / kCoopTileH);
+    const bool tile_src = c->coop_tile_src && npx * c->coop_threads == kTileW * kCoopTileH &&
+                          G == tiles;
     CoopState cs{dTi,      c->d_T64, c->d_T32, c->d_status,          c->d_stats,
                  d_T_out,  set,      set_next, c->d_head,            iters,
                  n_pairs,  G,        npx,      job ? job->depth : nullptr,
                  job ? job->out0 : 0, job && job->wait ? 1 : 0, wide ? 1 : 0,
-                 c->coop_res_host};
+                 c->coop_res_host, tile_src ? 1 : 0};
     const float4* recs = c->d_rec;
     size_t P = c->P;
     int W = c->W, H = c->H;
@@ -2650,6 +2673,8 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         // persistent fallback of run_iterations
         const char* crf = getenv("YOUTH_ICP_TEST_REFUSE_COOP");
         c->coop_refuse = crf && *crf && *crf != '0';
+        const char* cts = getenv("YOUTH_ICP_COOP_TILE_SRC");
+        if (cts && *cts == '0') c->coop_tile_src = false;
         const char* cmp = getenv("YOUTH_ICP_COOP_MAX_PAIRS");
         if (cmp && atoi(cmp) >= 0) c->coop_max_pairs = atoi(cmp);
     }
