@@ -71,7 +71,7 @@ def parse():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
-    ap.add_argument("--min-warmup-ms", type=float, default=50.0,
+    ap.add_argument("--min-warmup-ms", type=float, default=100.0,
                     help="after the --warmup steps, run more untimed steps until the warm-up has "
                          "lasted this long (the GPU's clock ramps over ~10-20 ms from idle; "
                          "reported as warmup_steps_run); 0 = exactly --warmup steps")
@@ -154,14 +154,19 @@ class Run:
             # clock has ramped up: the first timed window then ran 11 % below
             # the steady windows (profiles/r02/warm_probe.txt).  Same count on
             # every rank: a step holds the RCCL gather.
+            # one more step timed alone estimates a step (the first warm-up
+            # step also carries one-time setup)
             torch.cuda.synchronize()
-            el = time.perf_counter() - t0
-            need = a.min_warmup_ms * 1e-3 - el
-            extra = min(100000, math.ceil(need / (el / a.warmup))) if need > 0 else 0
+            t1 = time.perf_counter()
+            step()
+            torch.cuda.synchronize()
+            per = time.perf_counter() - t1
+            need = a.min_warmup_ms * 1e-3 - (time.perf_counter() - t0)
+            extra = min(100000, math.ceil(need / per)) if need > 0 else 0
             extra = int(self.max_over_ranks(float(extra)))
             for _ in range(extra):
                 step()
-            self.warmup_steps_run += extra
+            self.warmup_steps_run += 1 + extra
         ctx.set_timing(True, iteration_kernel_only=True)
         elapsed = self.window(step, a.steps)
         kt = {"k_icp": ctx.get_timing(0)}
@@ -466,51 +471,55 @@ def c5_rate(R, F=1000, sample_every=16, stream_frames=300, reps=3):
     return res
 
 
-def streamed_rate(a, frames, rel_batch):
+def streamed_rate(a, frames, rel_batch, passes=3):
     """The sequence streamed frame by frame from HOST memory through the
     tracker (processSlamFrame's worker path): per frame one 614 KB copy into
     pinned staging + H2D on a transfer stream, target prep of the new frame +
-    10 iterations against the previous one (one k_icp_coop launch), pose D2H.
-    `value`: pipelined two deep as the SLAM worker runs it
-    (youth_icp_track_submit / _collect: frame k+1's copy and H2D overlap frame
-    k's align); `sync_value`: youth_icp_track_frame, one frame at a time.
+    10 iterations against the previous one (one k_icp_coop launch), the pose
+    written into pinned memory by the kernel.  `value`: pipelined two deep as
+    the SLAM worker runs it (youth_icp_track_submit / _collect: frame k+1's
+    copy and H2D overlap frame k's align); `sync_value`: youth_icp_track_frame,
+    one frame at a time.  Median of `passes` passes each (host-side timing).
     Relative poses checked against the batch run's (fp32 output rounding) and
     the two modes against each other (bitwise)."""
     n = frames.shape[0]
     ctx = youth_icp.IcpContext(a.width, a.height, 2, iters=a.iters)
     ctx.track_frame(frames[0])
     ctx.track_frame(frames[1])                         # warm
-    ctx.track_reset()
-    t0 = time.perf_counter()
-    sync = []
-    for f in range(n):
-        T, st, has = ctx.track_frame(frames[f])
-        if has:
-            sync.append(T)
-    el_sync = time.perf_counter() - t0
-    ctx.track_reset()
-    t0 = time.perf_counter()
-    rel = []
-    for f in range(n):
-        ctx.track_submit(frames[f])
-        if ctx.track_pending() == 2:
+    r_sync, r_pipe = [], []
+    for _ in range(passes):
+        ctx.track_reset()
+        t0 = time.perf_counter()
+        sync = []
+        for f in range(n):
+            T, st, has = ctx.track_frame(frames[f])
+            if has:
+                sync.append(T)
+        r_sync.append(n / (time.perf_counter() - t0))
+        ctx.track_reset()
+        t0 = time.perf_counter()
+        rel = []
+        for f in range(n):
+            ctx.track_submit(frames[f])
+            if ctx.track_pending() == 2:
+                T, st, has = ctx.track_collect()
+                if has:
+                    rel.append(T)
+        while ctx.track_pending():
             T, st, has = ctx.track_collect()
             if has:
                 rel.append(T)
-    while ctx.track_pending():
-        T, st, has = ctx.track_collect()
-        if has:
-            rel.append(T)
-    el = time.perf_counter() - t0
+        r_pipe.append(n / (time.perf_counter() - t0))
     plan = ctx.get_plan()
     ctx.close()
-    return {"frames": n, "value": n / el, "unit": "frames/s", "us_per_frame": el / n * 1e6,
-            "sync_value": n / el_sync, "sync_us_per_frame": el_sync / n * 1e6,
-            "kernel_path": plan,
+    v, vs = float(np.median(r_pipe)), float(np.median(r_sync))
+    return {"frames": n, "value": v, "unit": "frames/s", "us_per_frame": 1e6 / v,
+            "sync_value": vs, "sync_us_per_frame": 1e6 / vs, "passes": passes,
+            "pass_values": r_pipe, "kernel_path": plan,
             "max_abs_diff_vs_batch_poses": pose_err(np.stack(rel), rel_batch[: n - 1]),
             "pipelined_equals_sync": bool(np.array_equal(np.stack(rel), np.stack(sync))),
-            "note": "host frames, copy to pinned + H2D + align + pose D2H per frame; value: two "
-                    "frames in flight (track_submit/collect), sync_value: track_frame"}
+            "note": "host frames, copy to pinned + H2D + align + pose to pinned per frame; value: "
+                    "two frames in flight (track_submit/collect), sync_value: track_frame"}
 
 
 def survey_noise_parity(a, ctx, main, n=16):
