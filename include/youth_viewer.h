@@ -57,6 +57,20 @@ int youth_cloud_build_device(youth_cloud_ctx* ctx, const int16_t* d_depth,
                              const youth_intrinsics* K, float* d_vertices,
                              int32_t* d_counts, void* stream);
 
+/* The same list in the WORLD frame, for a map view with the tracked poses
+ * (the device point buffer plus the pose overlay): frame f's
+ * camera-frame point P (the reference's x_pos, y_pos, z_pos) is moved by its
+ * camera -> world pose, d_T_world[f] (device, fp32 row-major 3x4 [R | t]; the
+ * first 12 entries of the SLAM trajectory's 4x4 T_w), as three fma chains
+ *   X_w = fma(R02, z, fma(R01, y, fma(R00, x, t0)))   (likewise Y_w, Z_w),
+ * the ICP transform's evaluation order, and the vertex is
+ * {-X_w, -Y_w, -Z_w, r, g, b} (the reference's display flip, :354).
+ * d_T_world NULL: exactly youth_cloud_build_device. */
+int youth_cloud_build_device_posed(youth_cloud_ctx* ctx, const int16_t* d_depth,
+                                   const uint8_t* d_rgb, int n_frames, int W, int H,
+                                   const youth_intrinsics* K, const float* d_T_world,
+                                   float* d_vertices, int32_t* d_counts, void* stream);
+
 /* One host frame: copies depth (and rgb) in, builds, copies the list out.
  * vertices: room for `cap` vertices (cap >= W*H always suffices).  Returns
  * the vertex count (>= 0) or a negative YOUTH_E* code; synchronous. */

@@ -375,6 +375,15 @@ int oracle_max_threads(void)
 int oracle_viewer_cloud(const int16_t* depth, const uint8_t* rgb, int W, int H,
                         const oracle_intrinsics* K, float* vertices)
 {
+    return oracle_viewer_cloud_posed(depth, rgb, W, H, K, NULL, vertices);
+}
+
+/* youth_cloud_build_device_posed (include/youth_viewer.h): the viewer's point
+ * moved by the camera -> world pose T (row-major 3x4) with the three fma
+ * chains of spec a7, then the display flip; T NULL: viewerModule.c:336-357. */
+int oracle_viewer_cloud_posed(const int16_t* depth, const uint8_t* rgb, int W, int H,
+                              const oracle_intrinsics* K, const float* T, float* vertices)
+{
     int n = 0;
     for (int y = 0; y < H; ++y) {
         for (int x = 0; x < W; ++x) {
@@ -385,9 +394,15 @@ int oracle_viewer_cloud(const int16_t* depth, const uint8_t* rgb, int W, int H,
                 const float xp = (((float)x - K->cx) * z) / K->fx;
                 const float yp = (((float)y - K->cy) * z) / K->fy;
                 float* o = vertices + (size_t)n * 6;
-                o[0] = -xp;
-                o[1] = -yp;
-                o[2] = -z;
+                if (T) {
+                    o[0] = -fmaf(T[2], z, fmaf(T[1], yp, fmaf(T[0], xp, T[3])));
+                    o[1] = -fmaf(T[6], z, fmaf(T[5], yp, fmaf(T[4], xp, T[7])));
+                    o[2] = -fmaf(T[10], z, fmaf(T[9], yp, fmaf(T[8], xp, T[11])));
+                } else {
+                    o[0] = -xp;
+                    o[1] = -yp;
+                    o[2] = -z;
+                }
                 o[3] = rgb ? (float)rgb[(size_t)index * 3 + 0] / 255.0f : 0.0f;
                 o[4] = rgb ? (float)rgb[(size_t)index * 3 + 1] / 255.0f : 0.0f;
                 o[5] = rgb ? (float)rgb[(size_t)index * 3 + 2] / 255.0f : 0.0f;

@@ -104,6 +104,8 @@ int oracle_max_threads(void);
  * (:349-352).  rgb may be NULL (colour 0).  Returns the vertex count. */
 int oracle_viewer_cloud(const int16_t* depth, const uint8_t* rgb, int W, int H,
                         const oracle_intrinsics* K, float* vertices);
+int oracle_viewer_cloud_posed(const int16_t* depth, const uint8_t* rgb, int W, int H,
+                              const oracle_intrinsics* K, const float* T, float* vertices);
 
 #ifdef __cplusplus
 }

@@ -55,6 +55,8 @@ def load_library() -> ctypes.CDLL:
     lib.oracle_max_threads.restype = c_int
     lib.oracle_viewer_cloud.argtypes = [P16, POINTER(ctypes.c_uint8), c_int, c_int, PK, PF]
     lib.oracle_viewer_cloud.restype = c_int
+    lib.oracle_viewer_cloud_posed.argtypes = [P16, POINTER(ctypes.c_uint8), c_int, c_int, PK, PF, PF]
+    lib.oracle_viewer_cloud_posed.restype = c_int
     for n in ("oracle_backproject", "oracle_normals", "oracle_associate", "oracle_reduce",
               "oracle_se3_exp", "oracle_align_batch"):
         getattr(lib, n).restype = None
@@ -88,16 +90,22 @@ def backproject(depth: np.ndarray, K=None):
     return X, Y, Z
 
 
-def viewer_cloud(depth: np.ndarray, rgb: np.ndarray | None = None, K=None) -> np.ndarray:
+def viewer_cloud(depth: np.ndarray, rgb: np.ndarray | None = None, K=None,
+                 T_world=None) -> np.ndarray:
     """display_3d_color's vertex list (viewerModule.c:336-357): [n_valid, 6]
-    float32 rows {-x, -y, -z, r, g, b} in raster order."""
+    float32 rows {-x, -y, -z, r, g, b} in raster order; with T_world (3x4 or
+    4x4 camera -> world) the points are moved to the world frame first
+    (youth_cloud_build_device_posed)."""
     d = np.ascontiguousarray(depth, np.int16)
     H, W = d.shape
     K = K_of(K) if K is not None else viewer_K(W, H)
     c = None if rgb is None else np.ascontiguousarray(rgb, np.uint8).reshape(H, W, 3)
+    T = None if T_world is None else np.ascontiguousarray(
+        np.asarray(T_world, np.float32).reshape(-1)[:12])
     out = np.zeros((H * W, 6), np.float32)
-    n = load_library().oracle_viewer_cloud(_p(d, c_int16), _p(c, ctypes.c_uint8), W, H,
-                                           ctypes.byref(K), _p(out, c_float))
+    n = load_library().oracle_viewer_cloud_posed(_p(d, c_int16), _p(c, ctypes.c_uint8), W, H,
+                                                 ctypes.byref(K), _p(T, c_float),
+                                                 _p(out, c_float))
     return out[:n].copy()
 
 

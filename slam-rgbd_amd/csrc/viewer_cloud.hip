@@ -182,7 +182,8 @@ __global__ __launch_bounds__(kCloudThreads) void k_cloud_scan(const int32_t* __r
 template <bool kVec, int kPx>
 __global__ __launch_bounds__(kCloudThreads) void k_cloud_emit(
     const int16_t* __restrict__ depth, const uint8_t* __restrict__ rgb, int W, int N, int tiles,
-    CloudK K, const int32_t* __restrict__ tile_off, float* __restrict__ vertices)
+    CloudK K, const int32_t* __restrict__ tile_off, const float* __restrict__ T_world,
+    float* __restrict__ vertices)
 {
     constexpr int kTile = kCloudThreads * kPx;
     __shared__ __align__(16) float stage[kTile * kVF + 4];   // the tile's vertices, list order
@@ -212,6 +213,12 @@ __global__ __launch_bounds__(kCloudThreads) void k_cloud_emit(
         total += sw[w];
     }
     int slot = woff + incl - c;
+    // frame f's camera -> world pose (row-major 3x4), or none
+    float Tw[12];
+    if (T_world) {
+#pragma unroll
+        for (int q = 0; q < 12; ++q) Tw[q] = T_world[(size_t)f * 12 + q];
+    }
     float* out = vertices + ((size_t)f * N + (size_t)tile_off[(size_t)f * tiles + tile]) * kVF;
     const int head = (int)(((uintptr_t)out >> 2) & 3);
     // (u, v) of pixel i; a thread's pixels may wrap rows (any W >= 1)
@@ -224,8 +231,13 @@ __global__ __launch_bounds__(kCloudThreads) void k_cloud_emit(
             const float z = (float)dd[k] / K.ds;
             const float x = (((float)u - K.cx) * z) / K.fx;
             const float y = (((float)v - K.cy) * z) / K.fy;
+            // world frame (youth_cloud_build_device_posed): P_w = R P + t as
+            // three fma chains, the ICP transform's order (spec a7)
+            const float px = T_world ? fmaf(Tw[2], z, fmaf(Tw[1], y, fmaf(Tw[0], x, Tw[3]))) : x;
+            const float py = T_world ? fmaf(Tw[6], z, fmaf(Tw[5], y, fmaf(Tw[4], x, Tw[7]))) : y;
+            const float pz = T_world ? fmaf(Tw[10], z, fmaf(Tw[9], y, fmaf(Tw[8], x, Tw[11]))) : z;
             // glVertex3f(-x_pos, -y_pos, -z_pos) (:354), glColor3f(r, g, b) (:349-351)
-            const float o[kVF] = {-x, -y, -z, (float)cc[3 * k + 0] / 255.0f,
+            const float o[kVF] = {-px, -py, -pz, (float)cc[3 * k + 0] / 255.0f,
                                   (float)cc[3 * k + 1] / 255.0f, (float)cc[3 * k + 2] / 255.0f};
 #pragma unroll
             for (int q = 0; q < kVF; ++q) stage[head + slot * kVF + q] = o[q];
@@ -365,6 +377,15 @@ int youth_cloud_build_device(youth_cloud_ctx* c, const int16_t* d_depth, const u
                              int n_frames, int W, int H, const youth_intrinsics* K,
                              float* d_vertices, int32_t* d_counts, void* stream)
 {
+    return youth_cloud_build_device_posed(c, d_depth, d_rgb, n_frames, W, H, K, nullptr,
+                                          d_vertices, d_counts, stream);
+}
+
+int youth_cloud_build_device_posed(youth_cloud_ctx* c, const int16_t* d_depth,
+                                   const uint8_t* d_rgb, int n_frames, int W, int H,
+                                   const youth_intrinsics* K, const float* d_T_world,
+                                   float* d_vertices, int32_t* d_counts, void* stream)
+{
     if (!c || !d_depth || !d_vertices || !d_counts)
         return cloud_error(YOUTH_EINVAL, "youth_cloud_build_device: null argument");
     if (n_frames < 0 || n_frames > c->max_frames || W < 1 || H < 1 || W > c->W || H > c->H ||
@@ -386,7 +407,7 @@ int youth_cloud_build_device(youth_cloud_ctx* c, const int16_t* d_depth, const u
                      (!d_rgb || ((uintptr_t)d_rgb % (c->px == 8 ? 8 : 4)) == 0);
     using CountFn = void (*)(const int16_t*, int, int, int32_t*);
     using EmitFn = void (*)(const int16_t*, const uint8_t*, int, int, int, CloudK, const int32_t*,
-                            float*);
+                            const float*, float*);
     static const CountFn count_fn[2][2] = {{k_cloud_count<false, 4>, k_cloud_count<true, 4>},
                                            {k_cloud_count<false, 8>, k_cloud_count<true, 8>}};
     static const EmitFn emit_fn[2][2] = {{k_cloud_emit<false, 4>, k_cloud_emit<true, 4>},
@@ -399,7 +420,7 @@ int youth_cloud_build_device(youth_cloud_ctx* c, const int16_t* d_depth, const u
     k_cloud_scan<<<n_frames, kCloudThreads, 0, s>>>(c->d_tile_cnt, tiles, c->d_tile_off, d_counts);
     CLOUD_TRY(hipGetLastError());
     hipLaunchKernelGGL(emit_fn[pi][vec], grid, dim3(kCloudThreads), 0, s, d_depth,
-                       d_rgb, W, N, tiles, k, (const int32_t*)c->d_tile_off, d_vertices);
+                       d_rgb, W, N, tiles, k, (const int32_t*)c->d_tile_off, d_T_world, d_vertices);
     CLOUD_TRY(hipGetLastError());
     return YOUTH_OK;
 }

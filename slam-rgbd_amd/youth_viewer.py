@@ -41,6 +41,10 @@ def load_library() -> ctypes.CDLL:
         lib.youth_cloud_build_device.restype = c_int
         lib.youth_cloud_build_device.argtypes = [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                                                  PI, c_void_p, c_void_p, c_void_p]
+        lib.youth_cloud_build_device_posed.restype = c_int
+        lib.youth_cloud_build_device_posed.argtypes = [c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                                       c_int, PI, c_void_p, c_void_p, c_void_p,
+                                                       c_void_p]
         lib.youth_cloud_build_host.restype = c_int
         lib.youth_cloud_build_host.argtypes = [c_void_p, POINTER(c_int16), POINTER(c_uint8), c_int,
                                                c_int, PI, POINTER(ctypes.c_float), c_int]
@@ -104,6 +108,16 @@ class CloudBuilder:
         _check(self._lib, self._lib.youth_cloud_build_device(
             self._ctx, d_depth, d_rgb or None, n_frames, W, H,
             None if K is None else ctypes.byref(K), d_vertices, d_counts, stream or None))
+
+    def build_device_posed(self, d_depth: int, d_rgb: int, n_frames: int, W: int, H: int,
+                           d_T_world: int, d_vertices: int, d_counts: int,
+                           K: Intrinsics | None = None, stream: int = 0) -> None:
+        """build_device in the world frame: d_T_world = device [n_frames][12]
+        fp32 row-major 3x4 camera -> world poses (0: camera frame)."""
+        _check(self._lib, self._lib.youth_cloud_build_device_posed(
+            self._ctx, d_depth, d_rgb or None, n_frames, W, H,
+            None if K is None else ctypes.byref(K), d_T_world or None, d_vertices, d_counts,
+            stream or None))
 
     def sync(self, stream: int = 0) -> None:
         _check(self._lib, self._lib.youth_cloud_sync(self._ctx, stream or None))

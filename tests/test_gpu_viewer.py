@@ -105,6 +105,51 @@ def test_cloud_device_batch(offset, px, monkeypatch):
         assert np.array_equal(_bits(verts[f, : counts[f]]), _bits(want))
 
 
+def _pose(rng, big=False):
+    """A random camera -> world pose, row-major 3x4 fp32."""
+    w = rng.normal(size=3) * (1.0 if big else 0.05)
+    th = np.linalg.norm(w)
+    Kx = np.array([[0, -w[2], w[1]], [w[2], 0, -w[0]], [-w[1], w[0], 0]]) / max(th, 1e-12)
+    R = np.eye(3) + np.sin(th) * Kx + (1 - np.cos(th)) * Kx @ Kx
+    t = rng.normal(size=3) * (5.0 if big else 0.1)
+    return np.hstack([R, t[:, None]]).astype(np.float32)
+
+
+@pytest.mark.parametrize("offset", [0, 1])
+def test_cloud_world_frame_batch(offset):
+    """youth_cloud_build_device_posed: every frame's points moved by its own
+    camera -> world pose (the tracker's trajectory), then the display flip;
+    bit-exact against the oracle with the same fma chains, small and large
+    poses, aligned and misaligned inputs; a null pose array is the camera
+    frame list."""
+    W, H, n = 320, 240, 4
+    rng = np.random.default_rng(5)
+    frames = [_frame(W, H, 200 + f) for f in range(n)]
+    T = np.stack([_pose(rng, big=f % 2 == 1) for f in range(n)])
+    d_all = torch.zeros(n * H * W + offset, dtype=torch.int16, device="cuda")
+    c_all = torch.zeros(n * H * W * 3 + offset, dtype=torch.uint8, device="cuda")
+    d_all[offset:] = torch.from_numpy(np.stack([f[0] for f in frames]).reshape(-1)).cuda()
+    c_all[offset:] = torch.from_numpy(np.stack([f[1] for f in frames]).reshape(-1)).cuda()
+    d_T = torch.from_numpy(T.reshape(n, 12)).cuda()
+    verts = torch.zeros((n, H * W, 6), dtype=torch.float32, device="cuda")
+    counts = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    with youth_viewer.CloudBuilder(W, H, max_frames=n) as cb:
+        cb.build_device_posed(d_all.data_ptr() + offset * 2, c_all.data_ptr() + offset, n, W, H,
+                              d_T.data_ptr(), verts.data_ptr(), counts.data_ptr(), stream=stream)
+        torch.cuda.synchronize()
+        got = verts.cpu().numpy(), counts.cpu().numpy()
+        cb.build_device_posed(d_all.data_ptr() + offset * 2, c_all.data_ptr() + offset, n, W, H,
+                              0, verts.data_ptr(), counts.data_ptr(), stream=stream)
+        torch.cuda.synchronize()
+        cam = verts.cpu().numpy()
+    for f, (d, c) in enumerate(frames):
+        want = oracle.viewer_cloud(d, c, T_world=T[f])
+        assert got[1][f] == want.shape[0]
+        assert np.array_equal(_bits(got[0][f, : got[1][f]]), _bits(want))
+        assert np.array_equal(_bits(cam[f, : got[1][f]]), _bits(oracle.viewer_cloud(d, c)))
+
+
 def test_cloud_rejects_bad_arguments():
     with youth_viewer.CloudBuilder(64, 48, max_frames=2) as cb:
         with pytest.raises(youth_icp.IcpError):

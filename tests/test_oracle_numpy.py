@@ -173,3 +173,23 @@ def test_numpy_restatement_equals_oracle_bitwise(case):
         assert np.array_equal(idx, oracle.associate(src, dst, T12, K, thr).ravel())
         assert np.array_equal(neq.view(np.uint64), oracle.reduce(src, dst, T12, K, thr).view(np.uint64))
         assert neq[28] > 0
+
+
+def test_world_frame_viewer_list_equals_numpy():
+    """oracle_viewer_cloud_posed (youth_cloud_build_device_posed's checker)
+    against the same three fma chains in numpy (fma32), bit for bit."""
+    src, _, _ = youth_synth.pairs(4, 1, 160, 120)
+    d = src[0]
+    K = oracle.viewer_K(160, 120)
+    th = 0.7
+    T = np.array([[np.cos(th), -np.sin(th), 0, 1.5], [np.sin(th), np.cos(th), 0, -2.0],
+                  [0, 0, 1, 0.25]], np.float32)
+    x, y, z = backproject_np(d, K)
+    m = (d > 0).ravel()
+    x, y, z = x.ravel()[m], y.ravel()[m], z.ravel()[m]
+    want = np.stack([-fma32(T[0, 2], z, fma32(T[0, 1], y, fma32(T[0, 0], x, T[0, 3]))),
+                     -fma32(T[1, 2], z, fma32(T[1, 1], y, fma32(T[1, 0], x, T[1, 3]))),
+                     -fma32(T[2, 2], z, fma32(T[2, 1], y, fma32(T[2, 0], x, T[2, 3])))], 1)
+    got = oracle.viewer_cloud(d, None, K, T_world=T)
+    assert np.array_equal(got[:, :3].view(np.uint32), want.view(np.uint32))
+    assert not got[:, 3:].any()
