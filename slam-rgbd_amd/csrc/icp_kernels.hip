@@ -1551,6 +1551,7 @@ constexpr int kCoopErrWord = kCoopMaxPairs * kCoopShards * kCoopShardStride;
 constexpr int kCoopPrepWords = kCoopErrWord + kCoopShardStride;
 constexpr int kCoopSetWords = kCoopPrepWords + kCoopMaxPairs * kCoopShardStride;
 constexpr int kCoopTileH = 24;  // fused prep tiles: 64 x 24 pixels (one per workgroup of a 640x480 pair: 200 tiles, G = 200)
+constexpr int kCoopTileHTall = 80;  // 64 x 80 (= 10 px per lane x 512: one per workgroup of a 1280x960 pair, G = 240)
 constexpr unsigned kCoopSpinMax = 1u << 22;  // polls (~1 us each): seconds, never reached
 
 struct CoopState {
@@ -1646,7 +1647,7 @@ __device__ __forceinline__ void coop_group(const float* __restrict__ X, const fl
 // of chunk c owns source pixels c kThreads npx + s kThreads + t, s < npx;
 // their back-projected X/Y/Z live in dynamic LDS [3][npx][kThreads] for the
 // whole launch.
-template <bool kFast, int kThreads>
+template <bool kFast, int kThreads, int kTH>
 __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restrict__ dsrc,
                                                              const float4* __restrict__ recs,
                                                              size_t P, PairMap pm, int W, int H,
@@ -1655,9 +1656,9 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
                                                              CoopState cs)
 {
     extern __shared__ float coop_src[];  // [3][npx][kThreads]
-    __shared__ float sPX[(kCoopTileH + 2) * kLdsW];  // fused prep neighbourhood
-    __shared__ float sPY[(kCoopTileH + 2) * kLdsW];
-    __shared__ float sPZ[(kCoopTileH + 2) * kLdsW];
+    __shared__ float sPX[(kTH + 2) * kLdsW];  // fused prep neighbourhood
+    __shared__ float sPY[(kTH + 2) * kLdsW];
+    __shared__ float sPZ[(kTH + 2) * kLdsW];
     __shared__ double red[kThreads / 64][kNeq];
     __shared__ double colsum[kSumCols][kPartStride];
     __shared__ double sh_neq[kNeq];
@@ -1699,17 +1700,17 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
     // one arrival on the pair's prep counter (R1 hand-off)
     if (cs.prep_src) {
         const int tiles_x = (W + kTileW - 1) / kTileW;
-        const int tiles = tiles_x * ((H + kCoopTileH - 1) / kCoopTileH);
+        const int tiles = tiles_x * ((H + kTH - 1) / kTH);
         const int16_t* tdep = cs.prep_src + (size_t)p * N;
         float4* R = const_cast<float4*>(recs) + (size_t)(cs.prep_out0 + p) * P;
         for (int t = c; t < tiles; t += G) {  // uniform per workgroup
             const int ty = t / tiles_x;
-            const int x0 = (t - ty * tiles_x) * kTileW, y0 = ty * kCoopTileH;
+            const int x0 = (t - ty * tiles_x) * kTileW, y0 = ty * kTH;
             if (cs.prep_wide)
-                prep_tile<kFast, true, true, kThreads, kCoopTileH>(tdep, R, W, H, P, K, F, nullptr,
+                prep_tile<kFast, true, true, kThreads, kTH>(tdep, R, W, H, P, K, F, nullptr,
                                                                    x0, y0, sPX, sPY, sPZ);
             else
-                prep_tile<kFast, false, true, kThreads, kCoopTileH>(tdep, R, W, H, P, K, F,
+                prep_tile<kFast, false, true, kThreads, kTH>(tdep, R, W, H, P, K, F,
                                                                     nullptr, x0, y0, sPX, sPY, sPZ);
             __syncthreads();  // LDS planes reused by the next tile
         }
@@ -1725,7 +1726,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
         const int base = c * npx * kThreads + threadIdx.x;
         const int tiles_x = (W + kTileW - 1) / kTileW;
         const int tyc = c / tiles_x;
-        const int tx0 = (c - tyc * tiles_x) * kTileW, ty0 = tyc * kCoopTileH;
+        const int tx0 = (c - tyc * tiles_x) * kTileW, ty0 = tyc * kTH;
         for (int s = 0; s < npx; ++s) {
             int u, v;
             bool inr;
@@ -1984,6 +1985,7 @@ struct youth_icp_ctx {
     int coop_launch = 0;             // YOUTH_ICP_COOP_LAUNCH: 0 serial (default), 1 runtime, 2 plain
     bool coop_refuse = false;        // YOUTH_ICP_TEST_REFUSE_COOP=1 (test hook)
     int coop_bpc[2][kCoopMaxPx + 1] = {};  // occupancy of k_icp_coop<fast> at npx (LDS)
+    int coop_bpc_tall[2] = {0, 0};          // the 64 x 80 prep-tile kernel at 10 px per lane
     unsigned* d_coop = nullptr;      // 2 counter sets of kCoopSetWords
     int32_t* d_status_out = nullptr; // [max_frames] host batch API: status per pair of the call
     int coop_par = 0;                // set used by the next coop call
@@ -2234,10 +2236,16 @@ static bool coop_plan(const youth_icp_ctx* c, int n_pairs, int* npx_out, int* G_
     return best >= 0;
 }
 
-static const void* coop_kernel(bool fast, int threads)
+static const void* coop_kernel(bool fast, int threads, bool tall = false)
 {
-    if (threads == 256) return fast ? (const void*)k_icp_coop<true, 256> : (const void*)k_icp_coop<false, 256>;
-    return fast ? (const void*)k_icp_coop<true, 512> : (const void*)k_icp_coop<false, 512>;
+    if (threads == 256)
+        return fast ? (const void*)k_icp_coop<true, 256, kCoopTileH>
+                    : (const void*)k_icp_coop<false, 256, kCoopTileH>;
+    if (tall)
+        return fast ? (const void*)k_icp_coop<true, 512, kCoopTileHTall>
+                    : (const void*)k_icp_coop<false, 512, kCoopTileHTall>;
+    return fast ? (const void*)k_icp_coop<true, 512, kCoopTileH>
+                : (const void*)k_icp_coop<false, 512, kCoopTileH>;
 }
 
 // Target frames to turn into records before (or, for the tracker, beside)
@@ -2276,9 +2284,10 @@ struct CoopOrder {
 };
 static CoopOrder g_coop_order[64];
 
-static int coop_enqueue(youth_icp_ctx* c, hipStream_t s, void** args, int blocks, int npx)
+static int coop_enqueue(youth_icp_ctx* c, hipStream_t s, void** args, int blocks, int npx,
+                        bool tall)
 {
-    const void* kern = coop_kernel(c->fast, c->coop_threads);
+    const void* kern = coop_kernel(c->fast, c->coop_threads, tall);
     const dim3 grid((unsigned)blocks), block(c->coop_threads);
     const unsigned lds = (unsigned)coop_lds(npx, c->coop_threads);
     if (c->coop_refuse)  // test hook: the runtime's refusal, nothing enqueued
@@ -2323,10 +2332,17 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
     c->coop_par ^= 1;
     const bool wide = job && (c->W % 4 == 0) && (reinterpret_cast<uintptr_t>(job->depth) % 8 == 0);
     // tile-shaped source chunks when one target tile is exactly one
-    // workgroup's pixels and the pair has one workgroup per tile
-    const int tiles = ((c->W + kTileW - 1) / kTileW) * ((c->H + kCoopTileH - 1) / kCoopTileH);
-    const bool tile_src = c->coop_tile_src && npx * c->coop_threads == kTileW * kCoopTileH &&
-                          G == tiles;
+    // workgroup's pixels and the pair has one workgroup per tile: 64 x 24
+    // tiles at 3 px per lane (640x480), 64 x 80 at 10 (1280x960; that
+    // kernel's larger prep LDS must still admit the planned grid)
+    auto tiles_of = [&](int th) {
+        return ((c->W + kTileW - 1) / kTileW) * ((c->H + th - 1) / th);
+    };
+    const bool tall = c->coop_tile_src && c->coop_threads == 512 &&
+                      npx * 512 == kTileW * kCoopTileHTall && G == tiles_of(kCoopTileHTall) &&
+                      (long long)n_pairs * G <= (long long)c->n_cu * c->coop_bpc_tall[c->fast ? 1 : 0];
+    const bool tile_src = tall || (c->coop_tile_src && npx * c->coop_threads == kTileW * kCoopTileH &&
+                                   G == tiles_of(kCoopTileH));
     CoopState cs{dTi,      c->d_T64, c->d_T32, c->d_status,          c->d_stats,
                  d_T_out,  set,      set_next, c->d_head,            iters,
                  n_pairs,  G,        npx,      job ? job->depth : nullptr,
@@ -2344,7 +2360,7 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
     EventPair ep{};
     rc = ev_begin(c, s, &ep, 0);
     if (rc) return rc;
-    rc = coop_enqueue(c, s, args, n_pairs * G, npx);
+    rc = coop_enqueue(c, s, args, n_pairs * G, npx, tall);
     if (rc) return rc;
     c->last_coop_G = G;
     c->last_coop_px = npx;
@@ -2662,6 +2678,14 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
                     return fail("occupancy coop", e);
                 c->coop_bpc[v][npx] = nb;
             }
+        for (int v = 0; v < 2; ++v) {
+            int nb = 0;
+            const int npx = kTileW * kCoopTileHTall / 512;
+            if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                     &nb, coop_kernel(v != 0, 512, true), 512, coop_lds(npx, 512))) != hipSuccess)
+                return fail("occupancy coop tall", e);
+            c->coop_bpc_tall[v] = nb;
+        }
         const char* nc = getenv("YOUTH_ICP_NO_COOP");
         c->coop = !(nc && *nc && *nc != '0');
         const char* cpx = getenv("YOUTH_ICP_COOP_PX");
