@@ -518,6 +518,7 @@ def streamed_rate(a, frames, rel_batch, passes=3):
             "pass_values": r_pipe, "kernel_path": plan,
             "max_abs_diff_vs_batch_poses": pose_err(np.stack(rel), rel_batch[: n - 1]),
             "pipelined_equals_sync": bool(np.array_equal(np.stack(rel), np.stack(sync))),
+            "in_flight": 2,
             "note": "host frames, copy to pinned + H2D + align + pose to pinned per frame; value: "
                     "two frames in flight (track_submit/collect), sync_value: track_frame"}
 

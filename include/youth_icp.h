@@ -289,15 +289,17 @@ int youth_icp_track_frame(youth_icp_ctx* ctx, const int16_t* depth,
  * (the caller's buffer is free on return), enqueues its H2D on a transfer
  * stream and its align (against the frame submitted before it) on the
  * context's stream, and returns without waiting, so the next frame's copy
- * overlaps this frame's align.  At most 2 frames may be in flight
- * (YOUTH_EINVAL otherwise).  youth_icp_track_collect waits for the OLDEST
+ * overlaps the aligns in flight.  At most YOUTH_TRACK_MAX_IN_FLIGHT frames
+ * may be in flight (YOUTH_EINVAL otherwise); with 3 in flight the next
+ * frame's host copy and H2D hide behind two aligns.  youth_icp_track_collect waits for the OLDEST
  * submitted frame and returns exactly what youth_icp_track_frame would have
  * returned for it (status bits or a negative code, T_rel, *has_ref).
  * youth_icp_track_frame = submit + collect, with nothing in flight. */
+#define YOUTH_TRACK_MAX_IN_FLIGHT 3
 int youth_icp_track_submit(youth_icp_ctx* ctx, const int16_t* depth,
                            const double* T_init);
 int youth_icp_track_collect(youth_icp_ctx* ctx, double* T_rel, int* has_ref);
-/* Frames submitted and not yet collected (0, 1 or 2). */
+/* Frames submitted and not yet collected (0 .. YOUTH_TRACK_MAX_IN_FLIGHT). */
 int youth_icp_track_pending(const youth_icp_ctx* ctx);
 
 /* Forget the reference frame (next tracked frame starts a new sequence). */

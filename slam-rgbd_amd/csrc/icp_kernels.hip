@@ -56,6 +56,9 @@ namespace {
 constexpr int kTileW = 64;
 constexpr int kTileH = 24;  // k_prep tiles 64 x 24 (16: 651 us, 24: 629 us, 32: 739 us per 512 frames; profiles/r02/ab_s13_prep_tiles.txt)
 constexpr int kPrepThreads = 256;
+// frames in flight through youth_icp_track_submit (YOUTH_TRACK_MAX_IN_FLIGHT):
+// with 3, frame k+1's host copy and H2D overlap frames k-1 and k's aligns
+constexpr int kTrackDepth = YOUTH_TRACK_MAX_IN_FLIGHT;
 constexpr int kLdsW = kTileW + 2;
 constexpr int kLdsH = kTileH + 2;
 
@@ -1999,15 +2002,16 @@ struct youth_icp_ctx {
     int track_ref = -1;  // ring slot (0/1) of the tracker's reference frame
     double* coop_res_host = nullptr;  // set around a tracker align: k_icp_coop writes its result there
     bool coop_tile_src = true;        // YOUTH_ICP_COOP_TILE_SRC=0: contiguous source chunks
-    // pipelined tracking (youth_icp_track_submit / _collect): up to two frames
-    // in flight, each with a pinned staging buffer, pinned results and events
+    // pipelined tracking (youth_icp_track_submit / _collect): up to
+    // kTrackDepth frames in flight, each with a pinned staging buffer, pinned
+    // results and events
     struct TrackSlot {
         int16_t* pinned = nullptr;     // host depth copy, H2D source
         double* res = nullptr;         // pinned: T64 [16], then the status word
         hipEvent_t h2d = nullptr;      // staging -> device depth done (xfer)
         hipEvent_t done = nullptr;     // align + result D2H done (stream)
         int has_ref = 0;
-    } trk[2];
+    } trk[kTrackDepth];
     hipEvent_t trk_depth_free[2] = {nullptr, nullptr};  // last align reading depth slot d
     int trk_head = 0, trk_n = 0;       // oldest in-flight submission, count in flight
 
@@ -3203,7 +3207,7 @@ int youth_icp_align_batch_multi(const int16_t* src, const int16_t* dst, int n_pa
 // Lazily: the transfer stream, two pinned staging/result slots and events.
 static int ensure_track(youth_icp_ctx* c)
 {
-    if (c->trk[1].done) return YOUTH_OK;
+    if (c->trk[kTrackDepth - 1].done) return YOUTH_OK;
     if (!c->xfer) HIP_TRY(hipStreamCreateWithFlags(&c->xfer, hipStreamNonBlocking));
     for (auto& q : c->trk) {
         if (!q.pinned)
@@ -3225,8 +3229,9 @@ static int ensure_track(youth_icp_ctx* c)
 int youth_icp_track_submit(youth_icp_ctx* c, const int16_t* depth, const double* T_init)
 {
     if (!c || !depth) return set_error(YOUTH_EINVAL, "track_submit: bad arguments");
-    if (c->trk_n >= 2)
-        return set_error(YOUTH_EINVAL, "track_submit: two frames in flight (collect one first)");
+    if (c->trk_n >= kTrackDepth)
+        return set_error(YOUTH_EINVAL, "track_submit: %d frames in flight (collect one first)",
+                         kTrackDepth);
     if (T_init)
         for (int i = 0; i < 16; ++i)
             if (!std::isfinite(T_init[i]))
@@ -3237,7 +3242,7 @@ int youth_icp_track_submit(youth_icp_ctx* c, const int16_t* depth, const double*
     if (rc) return rc;
     hipStream_t s = c->stream;
     const size_t N = c->N;
-    auto& q = c->trk[(c->trk_head + c->trk_n) & 1];
+    auto& q = c->trk[(c->trk_head + c->trk_n) % kTrackDepth];
     // the new frame goes to the ring slot that is not the reference; its depth
     // was last read (as a source) by the align two submissions back
     const int slot = c->track_ref == 0 ? 1 : 0;
@@ -3289,7 +3294,7 @@ int youth_icp_track_collect(youth_icp_ctx* c, double* T_rel, int* has_ref)
     int rc = bind_device(c);
     if (rc) return rc;
     auto& q = c->trk[c->trk_head];
-    c->trk_head ^= 1;
+    c->trk_head = (c->trk_head + 1) % kTrackDepth;
     --c->trk_n;
     HIP_TRY(hipEventSynchronize(q.done));
     if (has_ref) *has_ref = q.has_ref;

@@ -168,6 +168,9 @@ def _err(code: int) -> IcpError:
     return IcpError(code, (lib.youth_icp_last_error() or b"").decode())
 
 
+TRACK_MAX_IN_FLIGHT = 3   # YOUTH_TRACK_MAX_IN_FLIGHT (include/youth_icp.h)
+
+
 def _check(code: int) -> int:
     if code < 0:
         raise _err(code)
@@ -442,7 +445,8 @@ class IcpContext:
 
     def track_submit(self, depth: np.ndarray, T_init=None) -> None:
         """Pipelined tracking: enqueue one host frame (copied before the call
-        returns) and return without waiting; at most 2 in flight."""
+        returns) and return without waiting; at most TRACK_MAX_IN_FLIGHT in
+        flight."""
         d, Ti = self._frame_args(depth, T_init)
         _check(self._lib.youth_icp_track_submit(self._ctx, _p(d, c_int16), _p(Ti, c_double)))
 

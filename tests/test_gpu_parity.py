@@ -403,7 +403,7 @@ def test_track_submit_collect_pipelined():
         with pytest.raises(youth_icp.IcpError):
             ctx.track_collect()                              # nothing in flight
         got = []
-        order = "SCSSCCSSCSCSCSCSCC"   # S = submit next frame, C = collect oldest (<= 2 in flight)
+        order = "SCSSCCSSSCSCSCCSCC"   # S = submit next frame, C = collect oldest (<= 3 in flight)
         k = 0
         for op in order:
             if op == "S":
@@ -414,20 +414,20 @@ def test_track_submit_collect_pipelined():
         assert k == len(frames) and len(got) == len(frames) and ctx.track_pending() == 0
         for (Tg, sg, hg), (Tw, sw, hw) in zip(got, want):
             assert np.array_equal(Tg, Tw) and sg == sw and hg == hw
-        ctx.track_submit(frames[0])
-        ctx.track_submit(frames[1])
+        assert youth_icp.TRACK_MAX_IN_FLIGHT == 3
+        for f in range(3):
+            ctx.track_submit(frames[f])
         with pytest.raises(youth_icp.IcpError):
-            ctx.track_submit(frames[2])                      # a third frame in flight
+            ctx.track_submit(frames[3])                      # a fourth frame in flight
         with pytest.raises(youth_icp.IcpError):
-            ctx.track_frame(frames[2])                       # frames not collected
-        ctx.track_reset()                                    # frames 0 and 1 in flight
+            ctx.track_frame(frames[3])                       # frames not collected
+        ctx.track_reset()                                    # frames 0, 1 and 2 in flight
         _, _, h0 = ctx.track_collect()
-        ctx.track_submit(frames[2])
-        _, _, h1 = ctx.track_collect()
-        _, _, h2 = ctx.track_collect()
-        assert h0 and h1 and not h2                          # frame 2 starts a new sequence
-        T, st, has = ctx.track_frame(frames[3])
-        T64, _, sto, _ = oracle.align(frames[3], frames[2])
+        ctx.track_submit(frames[3])
+        hs = [h0] + [ctx.track_collect()[2] for _ in range(3)]
+        assert hs == [True, True, True, False]               # frame 3 starts a new sequence
+        T, st, has = ctx.track_frame(frames[4])
+        T64, _, sto, _ = oracle.align(frames[4], frames[3])
         assert has and st == sto and _pose_err(T, T64) <= POSE_TOL
 
 

@@ -21,9 +21,9 @@
 struct youth_icp_ctx {
     int W, H, has_ref;
     long long ref_sum;
-    /* submitted frames' results, oldest first (at most 2) */
-    double T[2][16];
-    int has[2], n, head;
+    /* submitted frames' results, oldest first */
+    double T[YOUTH_TRACK_MAX_IN_FLIGHT][16];
+    int has[YOUTH_TRACK_MAX_IN_FLIGHT], n, head;
 };
 
 int youth_icp_device_count(void) { return 1; }
@@ -52,8 +52,8 @@ static int stub_track(youth_icp_ctx* c, const int16_t* depth, double* T_rel, int
 int youth_icp_track_submit(youth_icp_ctx* c, const int16_t* depth, const double* T_init)
 {
     (void)T_init;
-    if (c->n >= 2) return YOUTH_EINVAL;
-    const int j = (c->head + c->n) & 1;
+    if (c->n >= YOUTH_TRACK_MAX_IN_FLIGHT) return YOUTH_EINVAL;
+    const int j = (c->head + c->n) % YOUTH_TRACK_MAX_IN_FLIGHT;
     stub_track(c, depth, c->T[j], &c->has[j]);
     ++c->n;
     return 0;
@@ -66,7 +66,7 @@ int youth_icp_track_collect(youth_icp_ctx* c, double* T_rel, int* has_ref)
     nanosleep(&ts, NULL);
     memcpy(T_rel, c->T[c->head], 16 * sizeof(double));
     if (has_ref) *has_ref = c->has[c->head];
-    c->head ^= 1;
+    c->head = (c->head + 1) % YOUTH_TRACK_MAX_IN_FLIGHT;
     --c->n;
     return 0;
 }

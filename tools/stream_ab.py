@@ -27,7 +27,7 @@ def main():
         t0 = time.perf_counter()
         for f in frames:
             ctx.track_submit(f)
-            if ctx.track_pending() == 2:
+            if ctx.track_pending() == int(os.environ.get("DEPTH", "2")):
                 ctx.track_collect()
         while ctx.track_pending():
             ctx.track_collect()
@@ -38,7 +38,7 @@ def main():
             ctx.track_frame(f)
         sync.append(len(frames) / (time.perf_counter() - t0))
     ctx.close()
-    print(f"{label:>8s} streamed two in flight: median {np.median(piped):8.0f} frames/s "
+    print(f"{label:>8s} streamed pipelined: median {np.median(piped):8.0f} frames/s "
           f"(min {min(piped):.0f} max {max(piped):.0f})  one at a time: median {np.median(sync):8.0f}",
           flush=True)
 
