@@ -54,8 +54,14 @@ namespace {
 // clamped fetch or a float4 load past N reads an invalid point (z = 0).
 // Sources are read straight from the caller's int16 depth.
 constexpr int kTileW = 64;
-constexpr int kTileH = 24;  // k_prep tiles 64 x 24 (16: 651 us, 24: 629 us, 32: 739 us per 512 frames; profiles/r02/ab_s13_prep_tiles.txt)
-constexpr int kPrepThreads = 256;
+// k_prep tiles 64 x 48 by 512-thread workgroups: four per CU fill all 32
+// wave slots (LDS 39.6 KB each) with 4 % halo rows.  Per 512 frames: 64 x 24
+// by 256 threads (seven per CU, LDS-limited) 617 us, 64 x 40 / 512 603 us,
+// 64 x 48 / 512 593 us, 64 x 80 and 64 x 96 by 1024 threads 625-643 us
+// (profiles/r02/ab_s44.txt, ab_s45.txt); fewer workgroups per CU cost more
+// (ab_s43.txt: 7 -> 6 per CU +8 %)
+constexpr int kTileH = 48;
+constexpr int kPrepThreads = 512;
 // frames in flight through youth_icp_track_submit (YOUTH_TRACK_MAX_IN_FLIGHT):
 // with 3, frame k+1's host copy and H2D overlap frames k-1 and k's aligns
 constexpr int kTrackDepth = YOUTH_TRACK_MAX_IN_FLIGHT;
