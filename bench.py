@@ -476,17 +476,19 @@ def streamed_rate(a, frames, rel_batch, passes=3):
     tracker (processSlamFrame's worker path): per frame one 614 KB copy into
     pinned staging + H2D on a transfer stream, target prep of the new frame +
     10 iterations against the previous one (one k_icp_coop launch), the pose
-    written into pinned memory by the kernel.  `value`: pipelined two deep as
-    the SLAM worker runs it (youth_icp_track_submit / _collect: frame k+1's
-    copy and H2D overlap frame k's align); `sync_value`: youth_icp_track_frame,
-    one frame at a time.  Median of `passes` passes each (host-side timing).
-    Relative poses checked against the batch run's (fp32 output rounding) and
-    the two modes against each other (bitwise)."""
+    written into pinned memory by the kernel.  `value`: the library's own
+    loop over a host sequence, two frames in flight as the SLAM worker runs
+    them (youth_icp_track_host_sequence: frame k+1's copy and H2D overlap
+    frame k's align); `python_pipelined_value`: the same through per-frame
+    youth_icp_track_submit / _collect calls from Python; `sync_value`:
+    youth_icp_track_frame, one frame at a time.  Median of `passes` passes
+    each (host-side timing).  Relative poses checked against the batch run's
+    (fp32 output rounding) and the three modes against each other (bitwise)."""
     n = frames.shape[0]
     ctx = youth_icp.IcpContext(a.width, a.height, 2, iters=a.iters)
     ctx.track_frame(frames[0])
     ctx.track_frame(frames[1])                         # warm
-    r_sync, r_pipe = [], []
+    r_sync, r_py, r_c = [], [], []
     for _ in range(passes):
         ctx.track_reset()
         t0 = time.perf_counter()
@@ -509,18 +511,24 @@ def streamed_rate(a, frames, rel_batch, passes=3):
             T, st, has = ctx.track_collect()
             if has:
                 rel.append(T)
-        r_pipe.append(n / (time.perf_counter() - t0))
+        r_py.append(n / (time.perf_counter() - t0))
+        ctx.track_reset()
+        t0 = time.perf_counter()
+        Tc, _ = ctx.track_host_sequence(frames)
+        r_c.append(n / (time.perf_counter() - t0))
     plan = ctx.get_plan()
     ctx.close()
-    v, vs = float(np.median(r_pipe)), float(np.median(r_sync))
+    v, vp, vs = float(np.median(r_c)), float(np.median(r_py)), float(np.median(r_sync))
     return {"frames": n, "value": v, "unit": "frames/s", "us_per_frame": 1e6 / v,
-            "sync_value": vs, "sync_us_per_frame": 1e6 / vs, "passes": passes,
-            "pass_values": r_pipe, "kernel_path": plan,
-            "max_abs_diff_vs_batch_poses": pose_err(np.stack(rel), rel_batch[: n - 1]),
-            "pipelined_equals_sync": bool(np.array_equal(np.stack(rel), np.stack(sync))),
+            "python_pipelined_value": vp, "sync_value": vs, "sync_us_per_frame": 1e6 / vs,
+            "passes": passes, "pass_values": r_c, "kernel_path": plan,
+            "max_abs_diff_vs_batch_poses": pose_err(Tc, rel_batch[: n - 1]),
+            "pipelined_equals_sync": bool(np.array_equal(np.stack(rel), np.stack(sync))
+                                          and np.array_equal(Tc, np.stack(sync))),
             "in_flight": 2,
             "note": "host frames, copy to pinned + H2D + align + pose to pinned per frame; value: "
-                    "two frames in flight (track_submit/collect), sync_value: track_frame"}
+                    "youth_icp_track_host_sequence (two in flight), python_pipelined_value: "
+                    "track_submit/collect from Python, sync_value: track_frame"}
 
 
 def survey_noise_parity(a, ctx, main, n=16):

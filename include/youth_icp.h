@@ -302,6 +302,15 @@ int youth_icp_track_collect(youth_icp_ctx* ctx, double* T_rel, int* has_ref);
 /* Frames submitted and not yet collected (0 .. YOUTH_TRACK_MAX_IN_FLIGHT). */
 int youth_icp_track_pending(const youth_icp_ctx* ctx);
 
+/* A recorded host sequence (frames [n_frames][H][W], e.g. a .bin playback)
+ * through the tracker, two frames in flight: the same results as
+ * youth_icp_track_frame on each frame in order (continuing from the
+ * reference the context holds).  T_rel [n][16] and status [n] (nullable)
+ * receive the frames that had a reference, in order; returns how many, or a
+ * negative YOUTH_E* code (nothing left in flight either way). */
+int youth_icp_track_host_sequence(youth_icp_ctx* ctx, const int16_t* frames, int n_frames,
+                                  double* T_rel, int32_t* status);
+
 /* Forget the reference frame (next tracked frame starts a new sequence). */
 void youth_icp_track_reset(youth_icp_ctx* ctx);
 

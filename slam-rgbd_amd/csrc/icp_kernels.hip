@@ -3323,6 +3323,44 @@ int youth_icp_track_pending(const youth_icp_ctx* c)
     return c ? c->trk_n : 0;
 }
 
+int youth_icp_track_host_sequence(youth_icp_ctx* c, const int16_t* frames, int n_frames,
+                                  double* T_rel, int32_t* status)
+{
+    if (!c || !frames || n_frames < 0 || !T_rel)
+        return set_error(YOUTH_EINVAL, "track_host_sequence: bad arguments");
+    if (c->trk_n) return set_error(YOUTH_EINVAL, "track_host_sequence: submitted frames not collected");
+    const size_t N = c->N;
+    int written = 0;
+    auto collect = [&]() -> int {
+        double T[16];
+        int has = 0;
+        const int st = youth_icp_track_collect(c, T, &has);
+        if (st < 0) return st;
+        if (has) {
+            memcpy(T_rel + (size_t)written * 16, T, sizeof(T));
+            if (status) status[written] = st;
+            ++written;
+        }
+        return YOUTH_OK;
+    };
+    for (int f = 0; f < n_frames; ++f) {
+        int rc = youth_icp_track_submit(c, frames + (size_t)f * N, nullptr);
+        if (rc == YOUTH_OK && c->trk_n == 2) rc = collect();  // two in flight, as the worker
+        if (rc) {
+            while (c->trk_n) (void)collect();
+            return rc;
+        }
+    }
+    while (c->trk_n) {
+        const int rc = collect();
+        if (rc) {
+            while (c->trk_n) (void)collect();
+            return rc;
+        }
+    }
+    return written;
+}
+
 int youth_icp_track_frame(youth_icp_ctx* c, const int16_t* depth, const double* T_init,
                           double* T_rel, int* has_ref)
 {

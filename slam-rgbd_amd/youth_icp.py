@@ -119,6 +119,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "youth_icp_track_submit": (c_int, [c_void_p, P16, PD]),
         "youth_icp_track_collect": (c_int, [c_void_p, PD, POINTER(c_int)]),
         "youth_icp_track_pending": (c_int, [c_void_p]),
+        "youth_icp_track_host_sequence": (c_int, [c_void_p, P16, c_int, PD, POINTER(c_int32)]),
         "youth_parse_camera_yaml": (c_int, [c_char_p, POINTER(Intrinsics), POINTER(c_int),
                                             POINTER(c_int)]),
         "youth_queue_create": (c_void_p, [c_int, c_int]),
@@ -460,6 +461,17 @@ class IcpContext:
 
     def track_pending(self) -> int:
         return int(self._lib.youth_icp_track_pending(self._ctx))
+
+    def track_host_sequence(self, frames: np.ndarray):
+        """youth_icp_track_host_sequence: (T_rel [m, 4, 4], status [m]) of the
+        frames that had a reference (m = n or n - 1)."""
+        f = np.ascontiguousarray(frames, np.int16).reshape(-1, self.H, self.W)
+        n = f.shape[0]
+        T = np.zeros((max(n, 1), 4, 4), np.float64)
+        st = np.zeros(max(n, 1), np.int32)
+        m = _check(self._lib.youth_icp_track_host_sequence(self._ctx, _p(f, c_int16), n,
+                                                           _p(T, c_double), _p(st, c_int32)))
+        return T[:m], st[:m]
 
 
 def selftest_projdiv(n: int, seed: int = 1, device: int = 0) -> tuple[int, int]:

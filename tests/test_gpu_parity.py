@@ -429,6 +429,14 @@ def test_track_submit_collect_pipelined():
         T, st, has = ctx.track_frame(frames[4])
         T64, _, sto, _ = oracle.align(frames[4], frames[3])
         assert has and st == sto and _pose_err(T, T64) <= POSE_TOL
+        # the library's own loop over a host sequence: the same results
+        ctx.track_reset()
+        Tseq, stseq = ctx.track_host_sequence(frames)
+        assert Tseq.shape[0] == len(frames) - 1 and ctx.track_pending() == 0
+        for k in range(len(frames) - 1):
+            assert np.array_equal(Tseq[k], want[k + 1][0]) and stseq[k] == want[k + 1][1]
+        Tmore, _ = ctx.track_host_sequence(frames[:2])       # continues from frame 8
+        assert Tmore.shape[0] == 2
 
 
 # ------------------------------------------------------- SLAM.h drop-in --
