@@ -2018,7 +2018,7 @@ struct youth_icp_ctx {
         hipEvent_t done = nullptr;     // align + result D2H done (stream)
         int has_ref = 0;
     } trk[kTrackDepth];
-    hipEvent_t trk_depth_free[2] = {nullptr, nullptr};  // last align reading depth slot d
+    int trk_slot_last[2] = {-1, -1};  // trk[] entry of the last align that read depth slot d
     int trk_head = 0, trk_n = 0;       // oldest in-flight submission, count in flight
 
     // host-buffer batch API: H2D of chunk k+1 on xfer overlaps the align of chunk k
@@ -2586,8 +2586,6 @@ void youth_icp_destroy(youth_icp_ctx* c)
         if (q.h2d) (void)hipEventDestroy(q.h2d);
         if (q.done) (void)hipEventDestroy(q.done);
     }
-    for (hipEvent_t e : c->trk_depth_free)
-        if (e) (void)hipEventDestroy(e);
     void* bufs[] = {c->d_depth, c->d_rec,   c->d_xyz,      c->d_T64, c->d_T32,   c->d_status,
                     c->d_Tinit, c->d_stats, c->d_partials, c->d_neq, c->d_assoc, c->d_Tout,
                     c->d_flag,  c->d_arrivals, c->d_arr_it, c->d_epoch, c->d_head,
@@ -3222,11 +3220,6 @@ static int ensure_track(youth_icp_ctx* c)
         if (!q.res) HIP_TRY(hipHostMalloc((void**)&q.res, 17 * sizeof(double), hipHostMallocDefault));
         if (!q.h2d) HIP_TRY(hipEventCreateWithFlags(&q.h2d, hipEventDisableTiming));
     }
-    for (auto& e : c->trk_depth_free)
-        if (!e) {
-            HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            HIP_TRY(hipEventRecord(e, c->stream));
-        }
     for (auto& q : c->trk)
         if (!q.done) HIP_TRY(hipEventCreateWithFlags(&q.done, hipEventDisableTiming));
     return YOUTH_OK;
@@ -3248,12 +3241,16 @@ int youth_icp_track_submit(youth_icp_ctx* c, const int16_t* depth, const double*
     if (rc) return rc;
     hipStream_t s = c->stream;
     const size_t N = c->N;
-    auto& q = c->trk[(c->trk_head + c->trk_n) % kTrackDepth];
+    const int qi = (c->trk_head + c->trk_n) % kTrackDepth;
+    auto& q = c->trk[qi];
     // the new frame goes to the ring slot that is not the reference; its depth
     // was last read (as a source) by the align two submissions back
     const int slot = c->track_ref == 0 ? 1 : 0;
     memcpy(q.pinned, depth, N * sizeof(int16_t));  // the caller's buffer is free on return
-    HIP_TRY(hipStreamWaitEvent(c->xfer, c->trk_depth_free[slot], 0));
+    // (that align's `done` event: one event record per frame, ~3 us each on
+    // the stream; profiles/r02/event_gap_s53.txt)
+    if (c->trk_slot_last[slot] >= 0)
+        HIP_TRY(hipStreamWaitEvent(c->xfer, c->trk[c->trk_slot_last[slot]].done, 0));
     HIP_TRY(hipMemcpyAsync(c->d_depth + (size_t)slot * N, q.pinned, N * sizeof(int16_t),
                            hipMemcpyHostToDevice, c->xfer));
     HIP_TRY(hipEventRecord(q.h2d, c->xfer));
@@ -3286,8 +3283,8 @@ int youth_icp_track_submit(youth_icp_ctx* c, const int16_t* depth, const double*
         (void)hipStreamSynchronize(c->xfer);
         return rc;
     }
-    HIP_TRY(hipEventRecord(c->trk_depth_free[slot], s));
     HIP_TRY(hipEventRecord(q.done, s));
+    c->trk_slot_last[slot] = qi;
     c->track_ref = slot;
     ++c->trk_n;
     return YOUTH_OK;
