@@ -308,6 +308,30 @@ def test_align_1280x960_20_iters():
         assert st == 0 and _pose_err(Tg[p], T64) <= POSE_TOL
 
 
+@pytest.mark.parametrize("tile_src", ["1", "0"])
+def test_single_pair_coop_tile_sources(tile_src, monkeypatch):
+    """C2 (640x480, 10 it) and C3 (1280x960, 20 it) single pairs through
+    k_icp_coop with tile-shaped source chunks (64x24 / 64x80 prep tiles, one
+    per workgroup) and with contiguous ones (YOUTH_ICP_COOP_TILE_SRC=0):
+    every fp64 pose within the bar of the oracle's, correspondence counts per
+    iteration equal to the oracle's."""
+    import torch
+    monkeypatch.setenv("YOUTH_ICP_COOP_TILE_SRC", tile_src)
+    for W, H, iters, G, px in ((640, 480, 10, 200, 3), (1280, 960, 20, 240, 10)):
+        src, dst, _ = youth_synth.pairs(31, 1, W, H)
+        ds, dd = torch.from_numpy(src).cuda(), torch.from_numpy(dst).cuda()
+        with youth_icp.IcpContext(W, H, 2, iters=iters) as ctx:
+            ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), 1)
+            T64, _, st = ctx.get_poses(1)
+            cnt, _ = ctx.get_stats(1, iters)
+            plan = ctx.get_plan()
+        assert plan["kernel"] == "k_icp_coop" and plan["workgroups_per_pair"] == G
+        assert plan["px_per_lane"] == px
+        To, _, sto, stats = oracle.align(src[0], dst[0], iters=iters)
+        assert st[0] == sto and _pose_err(T64[0], To) <= POSE_TOL
+        assert np.array_equal(cnt[0], stats[:, 0])
+
+
 @pytest.mark.parametrize("name", ["pair_80x60", "pair_160x120", "pair_97x53"])
 def test_align_matches_golden_pose(name):
     g = _load(name)
