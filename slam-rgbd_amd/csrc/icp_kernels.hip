@@ -1897,8 +1897,14 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
         const int32_t st = st_acc | (timeout ? YOUTH_STATUS_TIMEOUT : 0);
         if (i == 0) cs.status[p] = st;
         if (cs.res_host && p == 0) {
-            cs.res_host[i] = v;
-            if (i == 0) reinterpret_cast<int32_t*>(cs.res_host + 16)[0] = st;
+            // fine-grained pinned slot: system-scope stores go to host memory
+            // past the L2, and the wave waits for them before it ends, so the
+            // tracker's completion event needs no system-scope L2 writeback
+            __hip_atomic_store(cs.res_host + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (i == 0)
+                __hip_atomic_store(reinterpret_cast<int32_t*>(cs.res_host + 16), st,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __builtin_amdgcn_s_waitcnt(0);
         }
     }
 }
@@ -2016,6 +2022,9 @@ struct youth_icp_ctx {
         double* res = nullptr;         // pinned: T64 [16], then the status word
         hipEvent_t h2d = nullptr;      // staging -> device depth done (xfer)
         hipEvent_t done = nullptr;     // align + result D2H done (stream)
+        hipEvent_t done_nf = nullptr;  // the same without the system-scope fence (the
+                                       // kernel stored the result to host memory itself)
+        hipEvent_t ev = nullptr;       // the one of the two recorded for this submission
         int has_ref = 0;
     } trk[kTrackDepth];
     int trk_slot_last[2] = {-1, -1};  // trk[] entry of the last align that read depth slot d
@@ -2585,6 +2594,7 @@ void youth_icp_destroy(youth_icp_ctx* c)
         if (q.res) (void)hipHostFree(q.res);
         if (q.h2d) (void)hipEventDestroy(q.h2d);
         if (q.done) (void)hipEventDestroy(q.done);
+        if (q.done_nf) (void)hipEventDestroy(q.done_nf);
     }
     void* bufs[] = {c->d_depth, c->d_rec,   c->d_xyz,      c->d_T64, c->d_T32,   c->d_status,
                     c->d_Tinit, c->d_stats, c->d_partials, c->d_neq, c->d_assoc, c->d_Tout,
@@ -3211,17 +3221,22 @@ int youth_icp_align_batch_multi(const int16_t* src, const int16_t* dst, int n_pa
 // Lazily: the transfer stream, two pinned staging/result slots and events.
 static int ensure_track(youth_icp_ctx* c)
 {
-    if (c->trk[kTrackDepth - 1].done) return YOUTH_OK;
+    if (c->trk[kTrackDepth - 1].done_nf) return YOUTH_OK;
     if (!c->xfer) HIP_TRY(hipStreamCreateWithFlags(&c->xfer, hipStreamNonBlocking));
     for (auto& q : c->trk) {
         if (!q.pinned)
             HIP_TRY(hipHostMalloc((void**)&q.pinned, (size_t)c->N * sizeof(int16_t),
                                   hipHostMallocDefault));
-        if (!q.res) HIP_TRY(hipHostMalloc((void**)&q.res, 17 * sizeof(double), hipHostMallocDefault));
+        if (!q.res)
+            HIP_TRY(hipHostMalloc((void**)&q.res, 17 * sizeof(double), hipHostMallocCoherent));
         if (!q.h2d) HIP_TRY(hipEventCreateWithFlags(&q.h2d, hipEventDisableTiming));
     }
-    for (auto& q : c->trk)
+    for (auto& q : c->trk) {
         if (!q.done) HIP_TRY(hipEventCreateWithFlags(&q.done, hipEventDisableTiming));
+        if (!q.done_nf)
+            HIP_TRY(hipEventCreateWithFlags(&q.done_nf,
+                                            hipEventDisableTiming | hipEventDisableSystemFence));
+    }
     return YOUTH_OK;
 }
 
@@ -3250,7 +3265,7 @@ int youth_icp_track_submit(youth_icp_ctx* c, const int16_t* depth, const double*
     // (that align's `done` event: one event record per frame, ~3 us each on
     // the stream; profiles/r02/event_gap_s53.txt)
     if (c->trk_slot_last[slot] >= 0)
-        HIP_TRY(hipStreamWaitEvent(c->xfer, c->trk[c->trk_slot_last[slot]].done, 0));
+        HIP_TRY(hipStreamWaitEvent(c->xfer, c->trk[c->trk_slot_last[slot]].ev, 0));
     HIP_TRY(hipMemcpyAsync(c->d_depth + (size_t)slot * N, q.pinned, N * sizeof(int16_t),
                            hipMemcpyHostToDevice, c->xfer));
     HIP_TRY(hipEventRecord(q.h2d, c->xfer));
@@ -3283,7 +3298,10 @@ int youth_icp_track_submit(youth_icp_ctx* c, const int16_t* depth, const double*
         (void)hipStreamSynchronize(c->xfer);
         return rc;
     }
-    HIP_TRY(hipEventRecord(q.done, s));
+    // no result to publish (first frame) or k_icp_coop stored it to host
+    // memory itself: no system-scope fence; else the copies' result needs it
+    q.ev = (ref < 0 || c->last_coop) ? q.done_nf : q.done;
+    HIP_TRY(hipEventRecord(q.ev, s));
     c->trk_slot_last[slot] = qi;
     c->track_ref = slot;
     ++c->trk_n;
@@ -3299,7 +3317,7 @@ int youth_icp_track_collect(youth_icp_ctx* c, double* T_rel, int* has_ref)
     auto& q = c->trk[c->trk_head];
     c->trk_head = (c->trk_head + 1) % kTrackDepth;
     --c->trk_n;
-    HIP_TRY(hipEventSynchronize(q.done));
+    HIP_TRY(hipEventSynchronize(q.ev));
     if (has_ref) *has_ref = q.has_ref;
     if (!q.has_ref) {
         for (int i = 0; i < 16; ++i) T_rel[i] = (i % 5) == 0 ? 1.0 : 0.0;
