@@ -471,7 +471,7 @@ def c5_rate(R, F=1000, sample_every=16, stream_frames=300, reps=3):
     return res
 
 
-def streamed_rate(a, frames, rel_batch, passes=3):
+def streamed_rate(a, frames, rel_batch, passes=5):
     """The sequence streamed frame by frame from HOST memory through the
     tracker (processSlamFrame's worker path): per frame one 614 KB copy into
     pinned staging + H2D on a transfer stream, target prep of the new frame +
