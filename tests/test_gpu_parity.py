@@ -608,6 +608,32 @@ def test_plain_c_host_demo(tmp_path):
     assert np.allclose(rows[-1, 1:4], acc[:3, 3], atol=1e-6)
 
 
+def test_track_pipelined_copy_path(monkeypatch):
+    """The tracker through the persistent kernel (YOUTH_ICP_NO_COOP=1): the
+    result reaches the pinned slot by D2H copies and the frame's completion
+    event keeps its system-scope fence (the cooperative path stores the result
+    itself and records a fence-free event).  Two frames in flight equal
+    track_frame bit for bit; every pose is the oracle's (<= 1e-5)."""
+    monkeypatch.setenv("YOUTH_ICP_NO_COOP", "1")
+    frames, _ = youth_synth.sequence(5, 6)
+    with youth_icp.IcpContext(640, 480, 2) as ctx:
+        want = [ctx.track_frame(f) for f in frames]
+        assert ctx.get_plan()["kernel"] == PLAN["persistent"]
+        ctx.track_reset()
+        got = []
+        for f in frames:
+            ctx.track_submit(f)
+            if ctx.track_pending() == 2:
+                got.append(ctx.track_collect())
+        while ctx.track_pending():
+            got.append(ctx.track_collect())
+    for (Tg, sg, hg), (Tw, sw, hw) in zip(got, want):
+        assert np.array_equal(Tg, Tw) and sg == sw and hg == hw
+    for k in range(1, len(frames)):
+        T64, _, sto, _ = oracle.align(frames[k], frames[k - 1])
+        assert got[k][2] and got[k][1] == sto and _pose_err(got[k][0], T64) <= POSE_TOL
+
+
 PLAN = {"coop": "k_icp_coop", "persistent": "k_prep + k_icp (persistent)",
         "coop_refused": "k_prep + k_icp (persistent)",
         "per_iteration": "k_prep + k_init + k_reduce x iters (per-iteration)"}
