@@ -131,6 +131,21 @@ int youth_icp_device_count(void);
  * Environment YOUTH_ICP_NO_FASTDIV=1 forces the IEEE path. */
 int youth_icp_fastdiv_enabled(youth_icp_ctx* ctx);
 
+/* Arithmetic of spec a7/a8 (association, residual, Jacobian):
+ *   YOUTH_SPEC_FMA    fma chains and one correctly rounded reciprocal 1/P'z;
+ *   YOUTH_SPEC_SURVEY SURVEY.md §8a a7/a8 + §7 word for word: products and
+ *                     sums rounded separately in a fixed order (no FMA), the
+ *                     projection quotient fx P'x / P'z an IEEE division.
+ * Both are bit-exact (indices) against the oracle run in the same spec
+ * (oracle_set_spec).  youth_icp_set_spec selects one for the context's later
+ * aligns and returns the previous spec (EINVAL for another value); the
+ * environment YOUTH_ICP_SPEC=survey|fma sets a new context's (and therefore
+ * the SLAM.h worker's and the host batch API's) initial spec. */
+#define YOUTH_SPEC_FMA    0
+#define YOUTH_SPEC_SURVEY 1
+int youth_icp_set_spec(youth_icp_ctx* ctx, int spec);
+int youth_icp_get_spec(const youth_icp_ctx* ctx);
+
 /* One-shot host API:  aligns n_pairs independent pairs; src and
  * dst are [n_pairs][H][W] int16 host arrays.  T_out: [n_pairs][16] row-major
  * fp32 4x4 with P_dst = T * P_src.  assoc_out: nullable [n_pairs][H*W] int32
@@ -240,6 +255,15 @@ int youth_icp_get_plan(youth_icp_ctx* ctx, int* workgroups_per_pair, int* px_per
  * the IEEE reciprocal's on n pseudo-random (seeded) cases (must be 0). */
 int youth_icp_selftest_projdiv(int device, long long n, unsigned long long seed,
                                long long* bit_mismatches, long long* proj_mismatches);
+
+/* Validation of YOUTH_SPEC_SURVEY's projection quotient (the correctly
+ * rounded reciprocal plus ONE correction step) against IEEE num / den on n
+ * seeded cases: *quot_mismatches bitwise with den in [2^-60, 2^60], half of
+ * them next to a rounding midpoint; *proj_mismatches of the projected pixel
+ * floor((q + c) + 0.5) or its in-range test, den over the whole positive
+ * range.  Both must be 0. */
+int youth_icp_selftest_projquot(int device, long long n, unsigned long long seed,
+                                long long* quot_mismatches, long long* proj_mismatches);
 
 /* Self-test of the target-normal normalisation's fast path (correctly rounded
  * sqrt without rescaling, three quotients sharing one reciprocal) against

@@ -77,6 +77,25 @@ void oracle_normals(const float* X, const float* Y, const float* Z, int W, int H
     }
 }
 
+/* Which restatement of spec a7/a8 the association and residual follow
+ * (oracle_set_spec): ORACLE_SPEC_FMA, the build's default (fma
+ * chains, one correctly rounded reciprocal), or ORACLE_SPEC_SURVEY, SURVEY.md
+ * §8a a7/a8 and §7 word for word: separately rounded products and sums in a
+ * fixed order, no FMA, and the projection's quotient as an IEEE division,
+ * u' = floor(fx P'x / P'z + cx + 0.5) evaluated left to right.  Set before
+ * a run; read-only while one is in flight (OpenMP threads only read it). */
+static int g_spec = ORACLE_SPEC_FMA;
+
+int oracle_set_spec(int spec)
+{
+    if (spec != ORACLE_SPEC_FMA && spec != ORACLE_SPEC_SURVEY) return -1;
+    const int old = g_spec;
+    g_spec = spec;
+    return old;
+}
+
+int oracle_get_spec(void) { return g_spec; }
+
 /* Spec a7 for one source point.  Returns the target index or -1 and, when
  * matched, the transformed point q. */
 static inline int assoc_one(float sx, float sy, float sz, const float T[12],
@@ -86,23 +105,38 @@ static inline int assoc_one(float sx, float sy, float sz, const float T[12],
                             float thr2, float q[3])
 {
     if (!(sz > 0.0f)) return -1;
-    /* P' = R P + t as three fma chains (one rounding per step) */
-    const float qx = fmaf(T[2], sz, fmaf(T[1], sy, fmaf(T[0], sx, T[3])));
-    const float qy = fmaf(T[6], sz, fmaf(T[5], sy, fmaf(T[4], sx, T[7])));
-    const float qz = fmaf(T[10], sz, fmaf(T[9], sy, fmaf(T[8], sx, T[11])));
-    if (!(qz > 0.0f)) return -1;
-    /* one correctly rounded reciprocal, then fx P'x rz + (cx + 0.5) in one
-     * rounding (cx + 0.5 is exact: cx is a pixel coordinate) */
-    const float rz = 1.0f / qz;
-    const float fu = floorf(fmaf(K->fx * qx, rz, K->cx + 0.5f));
-    const float fv = floorf(fmaf(K->fy * qy, rz, K->cy + 0.5f));
+    float qx, qy, qz, fu, fv;
+    if (g_spec == ORACLE_SPEC_SURVEY) {
+        /* P' = R P + t, fp32, fixed op order, no FMA */
+        qx = ((T[0] * sx + T[1] * sy) + T[2] * sz) + T[3];
+        qy = ((T[4] * sx + T[5] * sy) + T[6] * sz) + T[7];
+        qz = ((T[8] * sx + T[9] * sy) + T[10] * sz) + T[11];
+        if (!(qz > 0.0f)) return -1;
+        /* u' = floor(fx P'x / P'z + cx + 0.5), the division kept a division
+         * (SURVEY §7 "never reciprocal-multiply"): the inverse of the viewer's
+         * x = ((u - cx) z) / fx (viewerModule.c:343-345) */
+        fu = floorf((((K->fx * qx) / qz) + K->cx) + 0.5f);
+        fv = floorf((((K->fy * qy) / qz) + K->cy) + 0.5f);
+    } else {
+        /* P' = R P + t as three fma chains (one rounding per step) */
+        qx = fmaf(T[2], sz, fmaf(T[1], sy, fmaf(T[0], sx, T[3])));
+        qy = fmaf(T[6], sz, fmaf(T[5], sy, fmaf(T[4], sx, T[7])));
+        qz = fmaf(T[10], sz, fmaf(T[9], sy, fmaf(T[8], sx, T[11])));
+        if (!(qz > 0.0f)) return -1;
+        /* one correctly rounded reciprocal, then fx P'x rz + (cx + 0.5) in one
+         * rounding (cx + 0.5 is exact: cx is a pixel coordinate) */
+        const float rz = 1.0f / qz;
+        fu = floorf(fmaf(K->fx * qx, rz, K->cx + 0.5f));
+        fv = floorf(fmaf(K->fy * qy, rz, K->cy + 0.5f));
+    }
     if (!(fu >= 0.0f && fu < (float)W && fv >= 0.0f && fv < (float)H)) return -1;
     const int j = (int)fv * W + (int)fu;
     const float tz = tZ[j];
     if (!(tz > 0.0f)) return -1;
     if (nX[j] == 0.0f && nY[j] == 0.0f && nZ[j] == 0.0f) return -1;
     const float dx = qx - tX[j], dy = qy - tY[j], dz = qz - tz;
-    const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+    const float d2 = g_spec == ORACLE_SPEC_SURVEY ? (dx * dx + dy * dy) + dz * dz
+                                                  : fmaf(dz, dz, fmaf(dy, dy, dx * dx));
     if (!(d2 < thr2)) return -1;
     q[0] = qx;
     q[1] = qy;
@@ -141,13 +175,20 @@ void oracle_reduce(const float* sX, const float* sY, const float* sZ,
         if (j < 0) continue;
         const float nx = nX[j], ny = nY[j], nz = nZ[j];
         const float dx = q[0] - tX[j], dy = q[1] - tY[j], dz = q[2] - tZ[j];
-        /* residual r = n . (P' - P_t)  (spec a8) */
-        const float r = fmaf(nz, dz, fmaf(ny, dy, nx * dx));
-        /* J = [ (P' x n)^T , n^T ]  for the left perturbation exp(xi) T */
-        float J[6];
-        J[0] = fmaf(q[1], nz, -(q[2] * ny));
-        J[1] = fmaf(q[2], nx, -(q[0] * nz));
-        J[2] = fmaf(q[0], ny, -(q[1] * nx));
+        /* residual r = n . (P' - P_t) and J = [ (P' x n)^T , n^T ] for the
+         * left perturbation exp(xi) T (spec a8) */
+        float r, J[6];
+        if (g_spec == ORACLE_SPEC_SURVEY) {
+            r = (nx * dx + ny * dy) + nz * dz;
+            J[0] = q[1] * nz - q[2] * ny;
+            J[1] = q[2] * nx - q[0] * nz;
+            J[2] = q[0] * ny - q[1] * nx;
+        } else {
+            r = fmaf(nz, dz, fmaf(ny, dy, nx * dx));
+            J[0] = fmaf(q[1], nz, -(q[2] * ny));
+            J[1] = fmaf(q[2], nx, -(q[0] * nz));
+            J[2] = fmaf(q[0], ny, -(q[1] * nx));
+        }
         J[3] = nx;
         J[4] = ny;
         J[5] = nz;
@@ -337,7 +378,7 @@ int oracle_align(const int16_t* src, const int16_t* dst, int W, int H,
 void oracle_align_batch(const int16_t* src, const int16_t* dst, int n_pairs,
                         int W, int H, const oracle_intrinsics* K, int iters,
                         float dist_thresh, double* T64, int32_t* status,
-                        int n_threads)
+                        double* stats, int n_threads)
 {
     const size_t N = (size_t)W * (size_t)H;
 #ifdef _OPENMP
@@ -353,7 +394,8 @@ void oracle_align_batch(const int16_t* src, const int16_t* dst, int n_pairs,
             float T32[12];
             status[p] = ws ? align_ws(src + (size_t)p * N, dst + (size_t)p * N, W, H,
                                       K, iters, dist_thresh, NULL,
-                                      T64 + (size_t)p * 16, T32, NULL, ws)
+                                      T64 + (size_t)p * 16, T32,
+                                      stats ? stats + (size_t)p * 2 * iters : NULL, ws)
                            : -1;
         }
         free(ws);

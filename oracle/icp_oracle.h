@@ -43,6 +43,20 @@ typedef struct oracle_intrinsics {
 
 #define ORACLE_NEQ 29
 
+/* Arithmetic of spec a7/a8 (association, residual, Jacobian):
+ *   ORACLE_SPEC_FMA    DESIGN.md §2, what the kernels run by default: fma
+ *                      chains and one correctly rounded reciprocal 1/P'z;
+ *   ORACLE_SPEC_SURVEY SURVEY.md §8a a7/a8 + §7 literally: no FMA (products
+ *                      and sums rounded separately, fixed order) and IEEE
+ *                      division fx P'x / P'z (youth_icp_set_spec's
+ *                      YOUTH_SPEC_SURVEY on the GPU).
+ * Back-projection, normals, reduction, solve and update are common.
+ * oracle_set_spec returns the previous spec (-1: unknown spec). */
+#define ORACLE_SPEC_FMA 0
+#define ORACLE_SPEC_SURVEY 1
+int oracle_set_spec(int spec);
+int oracle_get_spec(void);
+
 /* viewerModule.c:341-345 generalised.  Invalid pixel -> X=Y=Z=0. */
 void oracle_backproject(const int16_t* depth, int W, int H,
                         const oracle_intrinsics* K, float* X, float* Y, float* Z);
@@ -87,11 +101,12 @@ int oracle_align(const int16_t* src, const int16_t* dst, int W, int H,
                  double* stats);
 
 /* Batch of independent pairs, OpenMP over pairs with n_threads threads
- * (<= 0: all).  src/dst [n][H][W]; T64 [n][16]; status [n]. */
+ * (<= 0: all).  src/dst [n][H][W]; T64 [n][16]; status [n]; stats nullable
+ * [n][iters][2] (count, sum r^2 per iteration, as oracle_align). */
 void oracle_align_batch(const int16_t* src, const int16_t* dst, int n_pairs,
                         int W, int H, const oracle_intrinsics* K, int iters,
                         float dist_thresh, double* T64, int32_t* status,
-                        int n_threads);
+                        double* stats, int n_threads);
 
 /* Threads OpenMP will use for n_threads <= 0 (1 when built without OpenMP). */
 int oracle_max_threads(void);

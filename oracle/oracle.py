@@ -51,7 +51,10 @@ def load_library() -> ctypes.CDLL:
     lib.oracle_align.argtypes = [P16, P16, c_int, c_int, PK, c_int, c_float, PD, PD, PF, PD]
     lib.oracle_align.restype = c_int
     lib.oracle_align_batch.argtypes = [P16, P16, c_int, c_int, c_int, PK, c_int, c_float, PD,
-                                       PI32, c_int]
+                                       PI32, PD, c_int]
+    lib.oracle_set_spec.argtypes = [c_int]
+    lib.oracle_set_spec.restype = c_int
+    lib.oracle_get_spec.restype = c_int
     lib.oracle_max_threads.restype = c_int
     lib.oracle_viewer_cloud.argtypes = [P16, POINTER(ctypes.c_uint8), c_int, c_int, PK, PF]
     lib.oracle_viewer_cloud.restype = c_int
@@ -62,6 +65,39 @@ def load_library() -> ctypes.CDLL:
         getattr(lib, n).restype = None
     _lib = lib
     return lib
+
+
+SPEC_FMA = 0      # ORACLE_SPEC_FMA: DESIGN.md §2 (the kernels' default)
+SPEC_SURVEY = 1   # ORACLE_SPEC_SURVEY: SURVEY.md §8a a7/a8 + §7 literally
+SPECS = {"fma": SPEC_FMA, "survey": SPEC_SURVEY}
+
+
+def set_spec(spec) -> int:
+    """Select spec a7/a8's arithmetic ("fma" | "survey" or 0 | 1); returns the
+    previous one."""
+    code = SPECS.get(spec, spec)
+    old = load_library().oracle_set_spec(int(code))
+    if old < 0:
+        raise ValueError(f"unknown spec {spec!r}")
+    return old
+
+
+def get_spec() -> int:
+    return load_library().oracle_get_spec()
+
+
+class spec:
+    """Context manager: ``with oracle.spec("survey"): ...``."""
+
+    def __init__(self, name):
+        self.name = name
+
+    def __enter__(self):
+        self.old = set_spec(self.name)
+        return self
+
+    def __exit__(self, *exc):
+        set_spec(self.old)
 
 
 def K_of(K) -> OracleIntrinsics:
@@ -176,16 +212,21 @@ def align(src, dst, K=None, iters: int = 10, dist_thresh: float = 0.10, T_init=N
 
 
 def align_batch(src, dst, K=None, iters: int = 10, dist_thresh: float = 0.10,
-                n_threads: int = 0):
+                n_threads: int = 0, want_stats: bool = False):
+    """-> (T64 [n,4,4], status [n]) or, with want_stats, (T64, status, stats
+    [n, iters, 2] = per-iteration (count, sum r^2))."""
     s = np.ascontiguousarray(src, np.int16)
     d = np.ascontiguousarray(dst, np.int16)
     n, H, W = s.shape
     K = K_of(K) if K is not None else viewer_K(W, H)
     T = np.zeros((n, 4, 4), np.float64)
     st = np.zeros(n, np.int32)
+    stats = np.zeros((n, max(iters, 1), 2), np.float64) if want_stats else None
     load_library().oracle_align_batch(_p(s, c_int16), _p(d, c_int16), n, W, H, ctypes.byref(K),
                                       iters, dist_thresh, _p(T, c_double), _p(st, c_int32),
-                                      n_threads)
+                                      _p(stats, c_double), n_threads)
+    if want_stats:
+        return T, st, stats[:, :iters]
     return T, st
 
 

@@ -169,6 +169,31 @@ __device__ __forceinline__ float proj_rcp_rn(float den)
     return 1.0f / den;
 }
 
+// Which arithmetic spec a7/a8 runs in (youth_icp_set_spec):
+//   kSpecFma    fma chains and one correctly rounded reciprocal 1/P'z;
+//   kSpecSurvey SURVEY.md §8a a7/a8 + §7 literally: separately rounded
+//               products and sums in a fixed order (no FMA) and the
+//               projection quotient fx P'x / P'z as an IEEE division.
+// The oracle restates both (oracle_set_spec); every kernel of the iteration
+// (k_icp, k_icp_coop, k_reduce) is instantiated for each.
+constexpr int kSpecFma = YOUTH_SPEC_FMA;
+constexpr int kSpecSurvey = YOUTH_SPEC_SURVEY;
+
+// kSpecSurvey's projection quotient RN(n / den) from r = RN(1 / den)
+// (proj_recip inside proj_den_ok: correctly rounded, checked exhaustively):
+// q0 = RN(n r) is within one ulp of n / den, the remainder n - den q0 is
+// exact in one fma, and one correction q0 + (n - den q0) r rounds to
+// RN(n / den) (Markstein, IBM J. Res. Dev. 34(1), 1990, Theorem 1; barring
+// under/overflow of the remainder, which only happens for quotients that
+// project to the same pixel or off the frame).  hipcc's a/b applies two
+// such corrections; youth_icp_selftest_projquot compares this one with
+// IEEE a/b bitwise and through the projection (tests/test_gpu_parity.py).
+__device__ __forceinline__ float proj_quot(float n, float den, float r)
+{
+    const float q0 = n * r;
+    return fmaf(fmaf(-den, q0, n), r, q0);
+}
+
 // Spec a6's normalisation n = c / sqrtf(|c|^2) on its common range, bit for
 // bit.  hipcc's correctly rounded sqrtf is  x' = x < 2^-96 ? x 2^32 : x;
 // s = v_sqrt(x'); s -= (fma(-(s-1ulp), s, x') <= 0); s += (fma(-(s+1ulp), s,
@@ -294,6 +319,73 @@ __global__ void k_selftest_projdiv(unsigned long long n, unsigned long long seed
         const float uf = floorf(fmaf(num, proj_rcp_rn(den), c + 0.5f));
         const bool ii = (ui >= 0.0f) & (ui < 65536.0f), inf_ = (uf >= 0.0f) & (uf < 65536.0f);
         if (ii != inf_ || (ii && ui != uf)) ++b1;
+    }
+    if (b0) atomicAdd(bad + 0, b0);
+    if (b1) atomicAdd(bad + 1, b1);
+}
+
+// Self-test of kSpecSurvey's projection quotient (proj_quot with
+// proj_recip) against IEEE n / den:
+//   bad[0]: bitwise quotient mismatches over `n` SplitMix64 cases with den
+//           in the guard [2^-60, 2^60] and n of exponent in [-60, 60],
+//           half of them next to a rounding midpoint of n / den (n =
+//           RN(den (m + ulp(m)/2)) +- a few ulps);
+//   bad[1]: mismatches of the projected pixel floor((q + c) + 0.5) and its
+//           in-range test [0, 65536), den anywhere in the positive finite
+//           fp32 range (outside the guard the kernels divide with IEEE),
+//           c in [0, 4096): must be 0 for both.
+__device__ __forceinline__ float survey_quot(float n, float den)
+{
+    if (proj_den_ok(den)) return proj_quot(n, den, proj_recip(den));
+    return n / den;
+}
+__global__ void k_selftest_projquot(unsigned long long n, unsigned long long seed,
+                                    unsigned long long* bad)
+{
+    unsigned long long b0 = 0, b1 = 0;
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+    const unsigned long long tid = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    for (unsigned long long i = tid; i < n; i += stride) {
+        unsigned long long st = seed ^ (i * 0xD1B54A32D192ED03ull);
+        const unsigned long long r1 = sm64(st), r2 = sm64(st), r3 = sm64(st);
+        // guard-range quotient check
+        {
+            const int ed = (int)(r1 % 121) - 60;
+            const float den = __uint_as_float((unsigned)((ed + 127) << 23) | (unsigned)(r2 & 0x7FFFFF));
+            float num;
+            if (i & 1) {
+                const int em = (int)((r3 >> 40) % 41) - 20;
+                const float m = __uint_as_float((unsigned)((em + 127) << 23) | (unsigned)(r3 & 0x7FFFFF));
+                const double mid = (double)m + 0.5 * ((double)__uint_as_float(__float_as_uint(m) + 1u) - (double)m);
+                num = (float)((double)den * mid);
+                num = __uint_as_float(__float_as_uint(num) + (unsigned)((int)((r3 >> 23) & 7) - 3));
+            } else {
+                const int e = (int)((r3 >> 8) % 121) - 60;
+                num = __uint_as_float((unsigned)((e + 127) << 23) | (unsigned)(r3 & 0x7FFFFF) |
+                                      (unsigned)((r3 >> 63) << 31));
+            }
+            b0 += __float_as_uint(survey_quot(num, den)) != __float_as_uint(num / den);
+        }
+        // projected pixel, den over the whole positive range
+        {
+            const int ed = (i & 7) == 7 ? (int)(r2 % 254) - 126 : (int)(r2 % 121) - 60;
+            const float den = __uint_as_float((unsigned)((ed + 127) << 23) | (unsigned)(r1 & 0x7FFFFF));
+            float num;
+            if (i & 2) {
+                const float m = (float)((int)(r3 % 8192) - 4096) + 0.5f;
+                num = den * m;
+                num = __uint_as_float(__float_as_uint(num) + (unsigned)((int)((r3 >> 20) & 7) - 3));
+            } else {
+                const int e = (int)((r3 >> 8) % 161) - 80;
+                num = __uint_as_float((unsigned)((e + 127) << 23) | (unsigned)(r3 & 0x7FFFFF) |
+                                      (unsigned)((r3 >> 63) << 31));
+            }
+            const float c = (float)(r1 >> 52);
+            const float ui = floorf((num / den + c) + 0.5f);
+            const float uf = floorf((survey_quot(num, den) + c) + 0.5f);
+            const bool ii = (ui >= 0.0f) & (ui < 65536.0f), inf_ = (uf >= 0.0f) & (uf < 65536.0f);
+            if (ii != inf_ || (ii && ui != uf)) ++b1;
+        }
     }
     if (b0) atomicAdd(bad + 0, b0);
     if (b1) atomicAdd(bad + 1, b1);
@@ -925,17 +1017,43 @@ struct PoseState {
 //       u' = floor(fma(fx P'_x, rz, cx + 0.5)), v' likewise; in range of the
 //       target frame.  Unmatched pixels compute on safe values (branch-free)
 //       and gather record 0.
+//   kSpecSurvey: P'_i = ((R_i0 x + R_i1 y) + R_i2 z) + t_i and
+//       u' = floor(((fx P'_x) / P'_z + cx) + 0.5), the
+//       quotient IEEE (proj_quot on the shared correctly rounded reciprocal).
+template <int kSp>
 __device__ __forceinline__ void xform_project(const float* T, float sx, float sy, float sz,
                                               const Intr& K, int W, int H, float& qx, float& qy,
                                               float& qz, float& fu, float& fv, bool& in, int& j)
 {
-    qx = fmaf(T[2], sz, fmaf(T[1], sy, fmaf(T[0], sx, T[3])));
-    qy = fmaf(T[6], sz, fmaf(T[5], sy, fmaf(T[4], sx, T[7])));
-    qz = fmaf(T[10], sz, fmaf(T[9], sy, fmaf(T[8], sx, T[11])));
-    const bool vz = (sz > 0.0f) & (qz > 0.0f);
-    const float rz = proj_rcp_rn(vz ? qz : 1.0f);
-    const float uu = floorf(fmaf(K.fx * qx, rz, K.cx + 0.5f));
-    const float vv = floorf(fmaf(K.fy * qy, rz, K.cy + 0.5f));
+    float uu, vv;
+    bool vz;
+    if (kSp == kSpecSurvey) {
+        qx = ((T[0] * sx + T[1] * sy) + T[2] * sz) + T[3];
+        qy = ((T[4] * sx + T[5] * sy) + T[6] * sz) + T[7];
+        qz = ((T[8] * sx + T[9] * sy) + T[10] * sz) + T[11];
+        vz = (sz > 0.0f) & (qz > 0.0f);
+        const float den = vz ? qz : 1.0f;
+        const float nu = K.fx * qx, nv = K.fy * qy;
+        float pu, pv;
+        if (proj_den_ok(den)) {  // always in practice (den is a depth in metres)
+            const float r = proj_recip(den);
+            pu = proj_quot(nu, den, r);
+            pv = proj_quot(nv, den, r);
+        } else {
+            pu = nu / den;
+            pv = nv / den;
+        }
+        uu = floorf((pu + K.cx) + 0.5f);
+        vv = floorf((pv + K.cy) + 0.5f);
+    } else {
+        qx = fmaf(T[2], sz, fmaf(T[1], sy, fmaf(T[0], sx, T[3])));
+        qy = fmaf(T[6], sz, fmaf(T[5], sy, fmaf(T[4], sx, T[7])));
+        qz = fmaf(T[10], sz, fmaf(T[9], sy, fmaf(T[8], sx, T[11])));
+        vz = (sz > 0.0f) & (qz > 0.0f);
+        const float rz = proj_rcp_rn(vz ? qz : 1.0f);
+        uu = floorf(fmaf(K.fx * qx, rz, K.cx + 0.5f));
+        vv = floorf(fmaf(K.fy * qy, rz, K.cy + 0.5f));
+    }
     // 0 <= u' < W and 0 <= v' < H on the integer values: uu, vv are finite
     // integral floats (T finite, youth_icp.h), v_cvt_i32_f32 saturates
     // outside the int range, and a negative one wraps to >= 2^31 unsigned,
@@ -958,7 +1076,9 @@ __device__ __forceinline__ void xform_project(const float* T, float sx, float sy
 //       add.  Unmatched: the normal is masked to 0, so J = 0 and r = +-0 leave
 //       every sum unchanged.  The target's x, y are recomputed from its z with
 //       k_prep's expression (bit-identical to the stored plane).
-template <bool kFast>
+//   kSpecSurvey: d2 = (dx dx + dy dy) + dz dz, r = (n0 dx + n1 dy) + n2 dz,
+//       (P' x n)_0 = qy n2 - qz n1 etc. (no FMA).
+template <int kSp, bool kFast>
 __device__ __forceinline__ bool match_accumulate(float qx, float qy, float qz, f4v t, float fu,
                                                  float fv, bool in, const Intr& K,
                                                  const FastK& F, float thr2, double* acc)
@@ -967,14 +1087,22 @@ __device__ __forceinline__ bool match_accumulate(float qx, float qy, float qz, f
     const float tx = bp_div<kFast>((fu - K.cx) * tz, K.fx, F.hfx, F.lfx);
     const float ty = bp_div<kFast>((fv - K.cy) * tz, K.fy, F.hfy, F.lfy);
     const float dx = qx - tx, dy = qy - ty, dz = qz - tz;
-    const float d2 = fmaf(dz, dz, fmaf(dy, dy, dx * dx));
+    const float d2 = kSp == kSpecSurvey ? (dx * dx + dy * dy) + dz * dz
+                                        : fmaf(dz, dz, fmaf(dy, dy, dx * dx));
     const bool ok = in & (tz > 0.0f) & (d2 < thr2);
     const float n0 = ok ? t.y : 0.0f, n1 = ok ? t.z : 0.0f, n2 = ok ? t.w : 0.0f;
-    const float r = fmaf(n2, dz, fmaf(n1, dy, n0 * dx));
-    float Jf[6];
-    Jf[0] = fmaf(qy, n2, -(qz * n1));
-    Jf[1] = fmaf(qz, n0, -(qx * n2));
-    Jf[2] = fmaf(qx, n1, -(qy * n0));
+    float r, Jf[6];
+    if (kSp == kSpecSurvey) {
+        r = (n0 * dx + n1 * dy) + n2 * dz;
+        Jf[0] = qy * n2 - qz * n1;
+        Jf[1] = qz * n0 - qx * n2;
+        Jf[2] = qx * n1 - qy * n0;
+    } else {
+        r = fmaf(n2, dz, fmaf(n1, dy, n0 * dx));
+        Jf[0] = fmaf(qy, n2, -(qz * n1));
+        Jf[1] = fmaf(qz, n0, -(qx * n2));
+        Jf[2] = fmaf(qx, n1, -(qy * n0));
+    }
     Jf[3] = n0;
     Jf[4] = n1;
     Jf[5] = n2;
@@ -993,7 +1121,7 @@ __device__ __forceinline__ bool match_accumulate(float qx, float qy, float qz, f
 }
 
 // Accumulate source pixels [start, end) of one pair into acc (spec a7-a9).
-template <bool kAssoc, bool kFast, bool kAligned>
+template <int kSp, bool kAssoc, bool kFast, bool kAligned>
 __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
                                                  const float4* __restrict__ rec, int rec_bytes,
                                                  const float* __restrict__ T, int start, int end,
@@ -1038,7 +1166,8 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
                 v = wrap ? v + 1 : v;
                 backproject<kFast>((i + q) < end ? dd[q] : 0, u, v, K, F, sx, sy, sz);
             }
-            xform_project(T, sx, sy, sz, K, W, H, qx[q], qy[q], qz[q], fu[q], fv[q], in[q], j[q]);
+            xform_project<kSp>(T, sx, sy, sz, K, W, H, qx[q], qy[q], qz[q], fu[q], fv[q], in[q],
+                               j[q]);
         }
         u0 += stepU;
         v0 += stepV;
@@ -1054,8 +1183,8 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
                                                                                  0, 0));
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const bool ok = match_accumulate<kFast>(qx[q], qy[q], qz[q], t[q], fu[q], fv[q], in[q],
-                                                    K, F, thr2, acc);
+            const bool ok = match_accumulate<kSp, kFast>(qx[q], qy[q], qz[q], t[q], fu[q], fv[q],
+                                                         in[q], K, F, thr2, acc);
             if (kAssoc && (i + q) < end) arow[i + q] = ok ? j[q] : -1;
             cnt += ok ? 1 : 0;
         }
@@ -1135,7 +1264,7 @@ __device__ __forceinline__ void wave_reduce_scatter(const double* acc, int lane,
     total = v[0] + xchg_small<1>(v[0]);
 }
 
-template <bool kAssoc, bool kFast, bool kAligned, bool kFuse>
+template <int kSp, bool kAssoc, bool kFast, bool kAligned, bool kFuse>
 __global__ __launch_bounds__(kRedThreads) void k_reduce(
     const int16_t* __restrict__ dsrc, const float4* __restrict__ recs, size_t P, PairMap pm,
     int W, int H, Intr K, FastK F, float thr2, int chunk, double* __restrict__ partials,
@@ -1158,7 +1287,7 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce(
     const int start = b * chunk;
     const int end = min(start + chunk, N);
     int32_t* arow = kAssoc ? assoc + (size_t)p * N : nullptr;
-    accumulate_chunk<kAssoc, kFast, kAligned>(sD, rec, (int)(P * sizeof(float4)), T, start, end,
+    accumulate_chunk<kSp, kAssoc, kFast, kAligned>(sD, rec, (int)(P * sizeof(float4)), T, start, end,
                                               W, H, K, F, thr2, acc, arow);
     // wave reduce-scatter, then the four waves in fixed order through LDS
     const int wave = threadIdx.x >> 6;
@@ -1399,7 +1528,7 @@ __device__ __forceinline__ int icp_claim(const IterState& is, int item, int tota
 // thread 0 dequeues and claims the next item -> barrier.
 // (Dequeuing ahead from wave 1 so that waves 1-3 skip the second barrier
 // measured no faster: DESIGN.md §5.)
-template <bool kFast, bool kAligned>
+template <int kSp, bool kFast, bool kAligned>
 __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restrict__ dsrc,
                                                     const float4* __restrict__ recs, size_t P,
                                                     PairMap pm, int W, int H, Intr K, FastK F,
@@ -1446,7 +1575,7 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
         for (int q = 0; q < kNeq; ++q) acc[q] = 0.0;
         const int start = c * is.chunk;
         const int end = min(start + is.chunk, N);
-        accumulate_chunk<false, kFast, kAligned>(dsrc + (size_t)(pm.src0 + p) * N,
+        accumulate_chunk<kSp, false, kFast, kAligned>(dsrc + (size_t)(pm.src0 + p) * N,
                                                  recs + (size_t)(pm.tgt0 + p) * P,
                                                  (int)(P * sizeof(float4)), T, start, end, W, H,
                                                  K, F, thr2, acc, nullptr);
@@ -1619,7 +1748,7 @@ __device__ unsigned long long* coop_phase;
 // s0 .. s0+Q-1 of this lane in the LDS planes X/Y/Z [slot][256]): transform,
 // project, Q record gathers back to back, residual, Jacobian, exact products
 // into the fp64 accumulators.  Same expressions as accumulate_chunk.
-template <bool kFast, int Q, int kThreads>
+template <int kSp, bool kFast, int Q, int kThreads>
 __device__ __forceinline__ void coop_group(const float* __restrict__ X, const float* __restrict__ Y,
                                            const float* __restrict__ Z, int s0, const float* T,
                                            __amdgpu_buffer_rsrc_t rrec, int W, int H,
@@ -1635,7 +1764,7 @@ __device__ __forceinline__ void coop_group(const float* __restrict__ X, const fl
         const float sx = X[(s0 + q) * kThreads + t];
         const float sy = Y[(s0 + q) * kThreads + t];
         const float sz = Z[(s0 + q) * kThreads + t];
-        xform_project(T, sx, sy, sz, K, W, H, qx[q], qy[q], qz[q], fu[q], fv[q], in[q], j[q]);
+        xform_project<kSp>(T, sx, sy, sz, K, W, H, qx[q], qy[q], qz[q], fu[q], fv[q], in[q], j[q]);
     }
     f4v rec[Q];
 #pragma unroll
@@ -1643,8 +1772,8 @@ __device__ __forceinline__ void coop_group(const float* __restrict__ X, const fl
         rec[q] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rrec, j[q] * 16, 0, 0));
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-        const bool ok = match_accumulate<kFast>(qx[q], qy[q], qz[q], rec[q], fu[q], fv[q], in[q],
-                                                K, F, thr2, acc);
+        const bool ok = match_accumulate<kSp, kFast>(qx[q], qy[q], qz[q], rec[q], fu[q], fv[q],
+                                                     in[q], K, F, thr2, acc);
         nmatch += ok ? 1 : 0;
     }
 }
@@ -1656,7 +1785,7 @@ __device__ __forceinline__ void coop_group(const float* __restrict__ X, const fl
 // of chunk c owns source pixels c kThreads npx + s kThreads + t, s < npx;
 // their back-projected X/Y/Z live in dynamic LDS [3][npx][kThreads] for the
 // whole launch.
-template <bool kFast, int kThreads, int kTH>
+template <int kSp, bool kFast, int kThreads, int kTH>
 __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restrict__ dsrc,
                                                              const float4* __restrict__ recs,
                                                              size_t P, PairMap pm, int W, int H,
@@ -1805,11 +1934,11 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
         int nmatch = 0;
         int s0 = 0;
         for (; s0 + 4 <= npx; s0 += 4)
-            coop_group<kFast, 4, kThreads>(X, Y, Z, s0, T, rrec, W, H, K, F, thr2, acc, nmatch);
+            coop_group<kSp, kFast, 4, kThreads>(X, Y, Z, s0, T, rrec, W, H, K, F, thr2, acc, nmatch);
         switch (npx - s0) {  // wave-uniform tail
-        case 3: coop_group<kFast, 3, kThreads>(X, Y, Z, s0, T, rrec, W, H, K, F, thr2, acc, nmatch); break;
-        case 2: coop_group<kFast, 2, kThreads>(X, Y, Z, s0, T, rrec, W, H, K, F, thr2, acc, nmatch); break;
-        case 1: coop_group<kFast, 1, kThreads>(X, Y, Z, s0, T, rrec, W, H, K, F, thr2, acc, nmatch); break;
+        case 3: coop_group<kSp, kFast, 3, kThreads>(X, Y, Z, s0, T, rrec, W, H, K, F, thr2, acc, nmatch); break;
+        case 2: coop_group<kSp, kFast, 2, kThreads>(X, Y, Z, s0, T, rrec, W, H, K, F, thr2, acc, nmatch); break;
+        case 1: coop_group<kSp, kFast, 1, kThreads>(X, Y, Z, s0, T, rrec, W, H, K, F, thr2, acc, nmatch); break;
         default: break;
         }
         acc[28] = (double)nmatch;
@@ -1967,6 +2096,7 @@ struct youth_icp_ctx {
     Intr K{};
     FastK F{};
     bool fast = false;  // verified 2-op back-projection division
+    int spec = kSpecFma;  // spec a7/a8 arithmetic (youth_icp_set_spec, YOUTH_ICP_SPEC)
     youth_icp_params prm{};
     hipStream_t stream = nullptr;
 
@@ -1990,7 +2120,7 @@ struct youth_icp_ctx {
     unsigned* d_epoch = nullptr;     // [max_frames] persistent pose epochs
     unsigned* d_head = nullptr;      // queue words kQHead / kQError / kQSpins / kQWaited
     bool persistent = true;          // one k_icp launch per align (else per-iteration k_reduce)
-    int icp_blocks_per_cu[4] = {0, 0, 0, 0};  // occupancy of k_icp<fast, aligned>
+    int icp_blocks_per_cu[8] = {};  // occupancy of k_icp<spec, fast, aligned> [spec 4 + fast 2 + aligned]
     int n_cu = 0;
     // small batches: k_icp_coop (youth_icp_create reads the knobs)
     bool coop = true;                // YOUTH_ICP_NO_COOP=1 disables
@@ -1999,8 +2129,8 @@ struct youth_icp_ctx {
     int coop_max_pairs = kCoopMaxPairs;  // YOUTH_ICP_COOP_MAX_PAIRS (<= kCoopMaxPairs)
     int coop_launch = 0;             // YOUTH_ICP_COOP_LAUNCH: 0 serial (default), 1 runtime, 2 plain
     bool coop_refuse = false;        // YOUTH_ICP_TEST_REFUSE_COOP=1 (test hook)
-    int coop_bpc[2][kCoopMaxPx + 1] = {};  // occupancy of k_icp_coop<fast> at npx (LDS)
-    int coop_bpc_tall[2] = {0, 0};          // the 64 x 80 prep-tile kernel at 10 px per lane
+    int coop_bpc[4][kCoopMaxPx + 1] = {};  // occupancy of k_icp_coop<spec, fast> [spec 2 + fast] at npx (LDS)
+    int coop_bpc_tall[4] = {};              // the 64 x 80 prep-tile kernel at 10 px per lane
     unsigned* d_coop = nullptr;      // 2 counter sets of kCoopSetWords
     int32_t* d_status_out = nullptr; // [max_frames] host batch API: status per pair of the call
     int coop_par = 0;                // set used by the next coop call
@@ -2170,13 +2300,34 @@ static int launch_prep(youth_icp_ctx* c, hipStream_t s, const int16_t* depth, in
     return ev_end(c, s, &ep);
 }
 
-template <bool kAssoc, bool kFast, bool kAligned, bool kFuse>
+template <int kSp, bool kAssoc, bool kFast, bool kAligned, bool kFuse>
 static void launch_reduce_t(youth_icp_ctx* c, hipStream_t s, dim3 grid, const int16_t* dsrc,
                             PairMap pm, float thr2, int chunk, const PoseState& ps)
 {
-    hipLaunchKernelGGL((k_reduce<kAssoc, kFast, kAligned, kFuse>), grid, dim3(kRedThreads), 0, s,
-                       dsrc, c->d_rec, c->P, pm, c->W, c->H, c->K, c->F, thr2, chunk,
+    hipLaunchKernelGGL((k_reduce<kSp, kAssoc, kFast, kAligned, kFuse>), grid, dim3(kRedThreads), 0,
+                       s, dsrc, c->d_rec, c->P, pm, c->W, c->H, c->K, c->F, thr2, chunk,
                        c->d_partials, kAssoc ? c->d_assoc : (int32_t*)nullptr, ps);
+}
+
+// sel = assoc 8 | fuse 4 | fast 2 | aligned 1 (assoc with fuse excluded)
+template <int kSp>
+static void launch_reduce_sel(youth_icp_ctx* c, hipStream_t s, dim3 grid, const int16_t* dsrc,
+                              PairMap pm, float thr2, int chunk, const PoseState& ps, int sel)
+{
+    switch (sel) {
+    case 0: launch_reduce_t<kSp, false, false, false, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    case 1: launch_reduce_t<kSp, false, false, true, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    case 2: launch_reduce_t<kSp, false, true, false, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    case 3: launch_reduce_t<kSp, false, true, true, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    case 4: launch_reduce_t<kSp, false, false, false, true>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    case 5: launch_reduce_t<kSp, false, false, true, true>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    case 6: launch_reduce_t<kSp, false, true, false, true>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    case 7: launch_reduce_t<kSp, false, true, true, true>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    case 8: launch_reduce_t<kSp, true, false, false, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    case 9: launch_reduce_t<kSp, true, false, true, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    case 10: launch_reduce_t<kSp, true, true, false, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    default: launch_reduce_t<kSp, true, true, true, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
+    }
 }
 
 // fuse_it >= 0: fused solve of iteration fuse_it (k_reduce's last workgroup
@@ -2203,20 +2354,10 @@ static int launch_reduce(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, P
     const bool fuse = fuse_it >= 0;
     if (assoc && fuse) return set_error(YOUTH_EINVAL, "launch_reduce: assoc with fused solve");
     const int sel = (assoc ? 8 : 0) | (fuse ? 4 : 0) | (c->fast ? 2 : 0) | (aligned ? 1 : 0);
-    switch (sel) {
-    case 0: launch_reduce_t<false, false, false, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
-    case 1: launch_reduce_t<false, false, true, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
-    case 2: launch_reduce_t<false, true, false, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
-    case 3: launch_reduce_t<false, true, true, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
-    case 4: launch_reduce_t<false, false, false, true>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
-    case 5: launch_reduce_t<false, false, true, true>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
-    case 6: launch_reduce_t<false, true, false, true>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
-    case 7: launch_reduce_t<false, true, true, true>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
-    case 8: launch_reduce_t<true, false, false, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
-    case 9: launch_reduce_t<true, false, true, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
-    case 10: launch_reduce_t<true, true, false, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
-    default: launch_reduce_t<true, true, true, false>(c, s, grid, dsrc, pm, thr2, chunk, ps); break;
-    }
+    if (c->spec == kSpecSurvey)
+        launch_reduce_sel<kSpecSurvey>(c, s, grid, dsrc, pm, thr2, chunk, ps, sel);
+    else
+        launch_reduce_sel<kSpecFma>(c, s, grid, dsrc, pm, thr2, chunk, ps, sel);
     HIP_TRY(hipGetLastError());
     *nblk_out = nb;
     return ev_end(c, s, &ep);
@@ -2233,7 +2374,7 @@ static size_t coop_lds(int npx, int threads) { return (size_t)3 * npx * threads 
 static bool coop_plan(const youth_icp_ctx* c, int n_pairs, int* npx_out, int* G_out)
 {
     if (!c->coop || n_pairs > c->coop_max_pairs || n_pairs > kCoopMaxPairs) return false;
-    const int v = c->fast ? 1 : 0;
+    const int v = c->spec * 2 + (c->fast ? 1 : 0);
     long long best = -1;
     for (int npx = 1; npx <= kCoopMaxPx; ++npx) {
         if (c->coop_px && npx != c->coop_px) continue;
@@ -2255,16 +2396,23 @@ static bool coop_plan(const youth_icp_ctx* c, int n_pairs, int* npx_out, int* G_
     return best >= 0;
 }
 
-static const void* coop_kernel(bool fast, int threads, bool tall = false)
+template <int kSp>
+static const void* coop_kernel_t(bool fast, int threads, bool tall)
 {
     if (threads == 256)
-        return fast ? (const void*)k_icp_coop<true, 256, kCoopTileH>
-                    : (const void*)k_icp_coop<false, 256, kCoopTileH>;
+        return fast ? (const void*)k_icp_coop<kSp, true, 256, kCoopTileH>
+                    : (const void*)k_icp_coop<kSp, false, 256, kCoopTileH>;
     if (tall)
-        return fast ? (const void*)k_icp_coop<true, 512, kCoopTileHTall>
-                    : (const void*)k_icp_coop<false, 512, kCoopTileHTall>;
-    return fast ? (const void*)k_icp_coop<true, 512, kCoopTileH>
-                : (const void*)k_icp_coop<false, 512, kCoopTileH>;
+        return fast ? (const void*)k_icp_coop<kSp, true, 512, kCoopTileHTall>
+                    : (const void*)k_icp_coop<kSp, false, 512, kCoopTileHTall>;
+    return fast ? (const void*)k_icp_coop<kSp, true, 512, kCoopTileH>
+                : (const void*)k_icp_coop<kSp, false, 512, kCoopTileH>;
+}
+
+static const void* coop_kernel(int spec, bool fast, int threads, bool tall = false)
+{
+    return spec == kSpecSurvey ? coop_kernel_t<kSpecSurvey>(fast, threads, tall)
+                               : coop_kernel_t<kSpecFma>(fast, threads, tall);
 }
 
 // Target frames to turn into records before (or, for the tracker, beside)
@@ -2306,7 +2454,7 @@ static CoopOrder g_coop_order[64];
 static int coop_enqueue(youth_icp_ctx* c, hipStream_t s, void** args, int blocks, int npx,
                         bool tall)
 {
-    const void* kern = coop_kernel(c->fast, c->coop_threads, tall);
+    const void* kern = coop_kernel(c->spec, c->fast, c->coop_threads, tall);
     const dim3 grid((unsigned)blocks), block(c->coop_threads);
     const unsigned lds = (unsigned)coop_lds(npx, c->coop_threads);
     if (c->coop_refuse)  // test hook: the runtime's refusal, nothing enqueued
@@ -2359,7 +2507,7 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
     };
     const bool tall = c->coop_tile_src && c->coop_threads == 512 &&
                       npx * 512 == kTileW * kCoopTileHTall && G == tiles_of(kCoopTileHTall) &&
-                      (long long)n_pairs * G <= (long long)c->n_cu * c->coop_bpc_tall[c->fast ? 1 : 0];
+                      (long long)n_pairs * G <= (long long)c->n_cu * c->coop_bpc_tall[c->spec * 2 + (c->fast ? 1 : 0)];
     const bool tile_src = tall || (c->coop_tile_src && npx * c->coop_threads == kTileW * kCoopTileH &&
                                    G == tiles_of(kCoopTileH));
     CoopState cs{dTi,      c->d_T64, c->d_T32, c->d_status,          c->d_stats,
@@ -2384,6 +2532,19 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
     c->last_coop_G = G;
     c->last_coop_px = npx;
     return ev_end(c, s, &ep);
+}
+
+// k_icp<spec, fast, aligned> by index spec 4 + fast 2 + aligned
+typedef void (*IcpKernel)(const int16_t*, const float4*, size_t, PairMap, int, int, Intr, FastK,
+                          float, double*, IterState);
+static IcpKernel icp_kernel(int var)
+{
+    static const IcpKernel tab[8] = {
+        k_icp<kSpecFma, false, false>,    k_icp<kSpecFma, false, true>,
+        k_icp<kSpecFma, true, false>,     k_icp<kSpecFma, true, true>,
+        k_icp<kSpecSurvey, false, false>, k_icp<kSpecSurvey, false, true>,
+        k_icp<kSpecSurvey, true, false>,  k_icp<kSpecSurvey, true, true>};
+    return tab[var & 7];
 }
 
 // All ICP iterations of n_pairs pairs.  *exported is set when the kernel
@@ -2456,7 +2617,7 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
         rc = ensure_partials(c, (size_t)nb * n_pairs * kPartStride);
         if (rc) return rc;
         const bool aligned = (reinterpret_cast<uintptr_t>(dsrc) % 8 == 0) && (c->W % 4 == 0);
-        const int var = (c->fast ? 2 : 0) | (aligned ? 1 : 0);
+        const int var = c->spec * 4 + (c->fast ? 2 : 0) + (aligned ? 1 : 0);
         const long long items = (long long)iters * n_pairs * nb;
         long long grid = (long long)c->n_cu * c->icp_blocks_per_cu[var];
         if (grid > items) grid = items;
@@ -2470,8 +2631,7 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
         EventPair ep{};
         rc = ev_begin(c, s, &ep, 0);
         if (rc) return rc;
-        auto kern = c->fast ? (aligned ? k_icp<true, true> : k_icp<true, false>)
-                            : (aligned ? k_icp<false, true> : k_icp<false, false>);
+        auto kern = icp_kernel(var);
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kRedThreads), 0, s, dsrc, c->d_rec,
                            c->P, pm, c->W, c->H, c->K, c->F, thr2, c->d_partials, is);
         HIP_TRY(hipGetLastError());
@@ -2576,6 +2736,20 @@ int youth_icp_device_count(void)
 
 int youth_icp_fastdiv_enabled(youth_icp_ctx* c) { return c && c->fast ? 1 : 0; }
 
+int youth_icp_set_spec(youth_icp_ctx* c, int spec)
+{
+    if (!c || (spec != YOUTH_SPEC_FMA && spec != YOUTH_SPEC_SURVEY))
+        return set_error(YOUTH_EINVAL, "set_spec: bad arguments (%d)", spec);
+    const int old = c->spec;
+    c->spec = spec;
+    return old;
+}
+
+int youth_icp_get_spec(const youth_icp_ctx* c)
+{
+    return c ? c->spec : set_error(YOUTH_EINVAL, "get_spec: null context");
+}
+
 void youth_icp_destroy(youth_icp_ctx* c)
 {
     if (!c) return;
@@ -2674,12 +2848,10 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess)
             return fail("hipGetDeviceProperties", e);
         c->n_cu = prop.multiProcessorCount;
-        const void* kerns[4] = {(const void*)k_icp<false, false>, (const void*)k_icp<false, true>,
-                                (const void*)k_icp<true, false>, (const void*)k_icp<true, true>};
-        for (int v = 0; v < 4; ++v) {
+        for (int v = 0; v < 8; ++v) {
             int nb = 0;
-            if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kerns[v], kRedThreads, 0)) !=
-                hipSuccess)
+            if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                     &nb, (const void*)icp_kernel(v), kRedThreads, 0)) != hipSuccess)
                 return fail("occupancy", e);
             c->icp_blocks_per_cu[v] = nb > 0 ? nb : 1;
         }
@@ -2687,20 +2859,21 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         c->persistent = !(np && *np && *np != '0');
         const char* cth = getenv("YOUTH_ICP_COOP_THREADS");
         if (cth && atoi(cth) == 256) c->coop_threads = 256;
-        for (int v = 0; v < 2; ++v)
+        for (int v = 0; v < 4; ++v)
             for (int npx = 1; npx <= kCoopMaxPx; ++npx) {
                 int nb = 0;
                 if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                         &nb, coop_kernel(v != 0, c->coop_threads), c->coop_threads,
+                         &nb, coop_kernel(v >> 1, (v & 1) != 0, c->coop_threads), c->coop_threads,
                          coop_lds(npx, c->coop_threads))) != hipSuccess)
                     return fail("occupancy coop", e);
                 c->coop_bpc[v][npx] = nb;
             }
-        for (int v = 0; v < 2; ++v) {
+        for (int v = 0; v < 4; ++v) {
             int nb = 0;
             const int npx = kTileW * kCoopTileHTall / 512;
             if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                     &nb, coop_kernel(v != 0, 512, true), 512, coop_lds(npx, 512))) != hipSuccess)
+                     &nb, coop_kernel(v >> 1, (v & 1) != 0, 512, true), 512,
+                     coop_lds(npx, 512))) != hipSuccess)
                 return fail("occupancy coop tall", e);
             c->coop_bpc_tall[v] = nb;
         }
@@ -2719,6 +2892,10 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         if (cts && *cts == '0') c->coop_tile_src = false;
         const char* cmp = getenv("YOUTH_ICP_COOP_MAX_PAIRS");
         if (cmp && atoi(cmp) >= 0) c->coop_max_pairs = atoi(cmp);
+        // spec a7/a8 arithmetic: "survey" (SURVEY §8a literally) or "fma"
+        const char* sp = getenv("YOUTH_ICP_SPEC");
+        if (sp && strcmp(sp, "survey") == 0) c->spec = kSpecSurvey;
+        if (sp && strcmp(sp, "fma") == 0) c->spec = kSpecFma;
     }
     if ((e = hipMalloc(&c->d_coop, 2 * kCoopSetWords * sizeof(unsigned))) != hipSuccess)
         return fail("hipMalloc coop", e);
@@ -2867,6 +3044,31 @@ int youth_icp_selftest_projdiv(int device, long long n, unsigned long long seed,
     (void)hipFree(d_bad);
     if (e != hipSuccess) return set_error(YOUTH_EHIP, "selftest_projdiv: %s", hipGetErrorString(e));
     if (bit_mismatches) *bit_mismatches = (long long)h[0];
+    if (proj_mismatches) *proj_mismatches = (long long)h[1];
+    return YOUTH_OK;
+}
+
+int youth_icp_selftest_projquot(int device, long long n, unsigned long long seed,
+                                long long* quot_mismatches, long long* proj_mismatches)
+{
+    if (n < 0) return set_error(YOUTH_EINVAL, "selftest_projquot: n < 0");
+    const int ndev = youth_icp_device_count();
+    if (ndev <= 0 || device < 0 || device >= ndev)
+        return set_error(YOUTH_ENODEV, "selftest_projquot: no HIP device %d", device);
+    HIP_TRY(hipSetDevice(device));
+    unsigned long long* d_bad = nullptr;
+    HIP_TRY(hipMalloc(&d_bad, 2 * sizeof(unsigned long long)));
+    unsigned long long h[2] = {0, 0};
+    hipError_t e = hipMemset(d_bad, 0, sizeof(h));
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_selftest_projquot, dim3(4096), dim3(256), 0, 0,
+                           (unsigned long long)n, seed, d_bad);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(h, d_bad, sizeof(h), hipMemcpyDeviceToHost);
+    (void)hipFree(d_bad);
+    if (e != hipSuccess) return set_error(YOUTH_EHIP, "selftest_projquot: %s", hipGetErrorString(e));
+    if (quot_mismatches) *quot_mismatches = (long long)h[0];
     if (proj_mismatches) *proj_mismatches = (long long)h[1];
     return YOUTH_OK;
 }

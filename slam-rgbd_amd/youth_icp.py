@@ -34,6 +34,8 @@ YOUTH_ENOMEM = -2
 YOUTH_EHIP = -3
 YOUTH_ENODEV = -4
 YOUTH_NEQ = 29
+SPEC_FMA = 0       # YOUTH_SPEC_FMA: spec a7/a8 on fma chains
+SPEC_SURVEY = 1    # YOUTH_SPEC_SURVEY: SURVEY.md §8a a7/a8 as worded (no FMA, IEEE division)
 STATUS_DEGENERATE = 1
 STATUS_FEW_MATCHES = 2
 
@@ -83,6 +85,11 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "youth_icp_last_error": (c_char_p, []),
         "youth_icp_device_count": (c_int, []),
         "youth_icp_fastdiv_enabled": (c_int, [c_void_p]),
+        "youth_icp_set_spec": (c_int, [c_void_p, c_int]),
+        "youth_icp_get_spec": (c_int, [c_void_p]),
+        "youth_icp_selftest_projquot": (c_int, [c_int, ctypes.c_longlong, ctypes.c_ulonglong,
+                                                POINTER(ctypes.c_longlong),
+                                                POINTER(ctypes.c_longlong)]),
         "youth_icp_align_batch": (c_int, [P16, P16, c_int, c_int, c_int, POINTER(Intrinsics),
                                           c_int, PF, PI32]),
         "youth_icp_align_batch_multi": (c_int, [P16, P16, c_int, c_int, c_int,
@@ -292,7 +299,7 @@ class IcpContext:
     """Device workspace for W x H frames (youth_icp_create)."""
 
     def __init__(self, width: int, height: int, max_frames: int, K: Intrinsics | None = None,
-                 iters: int = 10, dist_thresh: float = 0.10, device: int = 0):
+                 iters: int = 10, dist_thresh: float = 0.10, device: int = 0, spec=None):
         self._lib = load_library()
         self.W, self.H, self.max_frames = width, height, max_frames
         self.K = K if K is not None else default_intrinsics(width, height)
@@ -302,6 +309,8 @@ class IcpContext:
         if not self._ctx:
             msg = (self._lib.youth_icp_last_error() or b"").decode()
             raise IcpError(YOUTH_ENODEV if "no HIP device" in msg else YOUTH_EHIP, msg)
+        if spec is not None:
+            self.spec = spec
 
     @property
     def handle(self) -> int:
@@ -311,6 +320,16 @@ class IcpContext:
     def fastdiv(self) -> bool:
         """True when the verified 3-op back-projection division is in use."""
         return bool(self._lib.youth_icp_fastdiv_enabled(self._ctx))
+
+    @property
+    def spec(self) -> int:
+        """Spec a7/a8 arithmetic of the next aligns (SPEC_FMA / SPEC_SURVEY)."""
+        return _check(self._lib.youth_icp_get_spec(self._ctx))
+
+    @spec.setter
+    def spec(self, value) -> None:
+        code = {"fma": SPEC_FMA, "survey": SPEC_SURVEY}.get(value, value)
+        _check(self._lib.youth_icp_set_spec(self._ctx, int(code)))
 
     def close(self):
         if getattr(self, "_ctx", None):
@@ -481,6 +500,15 @@ def selftest_projdiv(n: int, seed: int = 1, device: int = 0) -> tuple[int, int]:
     b, p = ctypes.c_longlong(0), ctypes.c_longlong(0)
     _check(lib.youth_icp_selftest_projdiv(device, n, seed, ctypes.byref(b), ctypes.byref(p)))
     return b.value, p.value
+
+
+def selftest_projquot(n: int, seed: int = 1, device: int = 0) -> tuple[int, int]:
+    """youth_icp_selftest_projquot: (quotient mismatches, projection mismatches)
+    of YOUTH_SPEC_SURVEY's projection quotient vs IEEE num / den on n cases."""
+    lib = load_library()
+    q, p = ctypes.c_longlong(0), ctypes.c_longlong(0)
+    _check(lib.youth_icp_selftest_projquot(device, n, seed, ctypes.byref(q), ctypes.byref(p)))
+    return q.value, p.value
 
 
 def selftest_normalize(n: int, seed: int = 1, device: int = 0) -> tuple[int, int, int]:

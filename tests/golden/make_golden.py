@@ -9,7 +9,13 @@ Provenance, case by case:
     vectors pinned to the REFERENCE; they are written out here verbatim.
   * pair_* / seq_* — inputs from the synthetic depth source
     (libyouth_synth.so), expected outputs from the C oracle
-    (oracle/liboracle.so).  The reference has no ICP, so
+    (oracle/liboracle.so) in its default spec (ORACLE_SPEC_FMA).
+  * survey/pair_* / survey/seq_* — the same cases with spec a7/a8 as
+    SURVEY.md §8a words it (ORACLE_SPEC_SURVEY: no FMA, IEEE division).  The
+    committed files are the round-1 fixtures, written by the round-1 oracle
+    before the fma spec existed (git 1041b06^:tests/golden/); `--survey`
+    regenerates them with today's oracle and must leave their arrays equal
+    (tests/test_oracle.py checks it without writing).  The reference has no ICP, so
     these pin this build's own spec against regressions: "parity unpinned"
     with respect to the reference beyond back-projection.
 
@@ -44,7 +50,7 @@ def scaled_K(W, H):
                                    float(H // 2), 1000.0)
 
 
-def make_pair_case(name, W, H, index, iters=10, dist=0.10):
+def make_pair_case(name, W, H, index, iters=10, dist=0.10, out=HERE):
     K = scaled_K(W, H)
     src, dst, Tgt = youth_synth.pairs(index, 1, W, H, K=_yk(K))
     src, dst = src[0], dst[0]
@@ -57,7 +63,7 @@ def make_pair_case(name, W, H, index, iters=10, dist=0.10):
     T64, T32, st, stats = oracle.align(src, dst, K, iters, dist)
     idxF = oracle.associate(src, dst, T32, K, dist)
     np.savez_compressed(
-        os.path.join(HERE, name + ".npz"), src=src, dst=dst,
+        os.path.join(out, name + ".npz"), src=src, dst=dst,
         K=np.array([K.fx, K.fy, K.cx, K.cy, K.depth_scale], np.float32),
         iters=np.int32(iters), dist_thresh=np.float32(dist), T_gt=Tgt[0],
         src_xyz=np.stack([sX, sY, sZ]), dst_xyz=np.stack([tX, tY, tZ]),
@@ -72,14 +78,14 @@ def _yk(K):
     return Intrinsics(K.fx, K.fy, K.cx, K.cy, K.depth_scale)
 
 
-def make_seq_case(name, W, H, n_frames, iters=10, dist=0.10):
+def make_seq_case(name, W, H, n_frames, iters=10, dist=0.10, out=HERE):
     K = scaled_K(W, H)
     frames, Twc = youth_synth.sequence(0, n_frames, W, H, K=_yk(K))
     rel = []
     for k in range(n_frames - 1):
         T64, T32, st, _ = oracle.align(frames[k + 1], frames[k], K, iters, dist)
         rel.append(T64)
-    np.savez_compressed(os.path.join(HERE, name + ".npz"), frames=frames,
+    np.savez_compressed(os.path.join(out, name + ".npz"), frames=frames,
                         K=np.array([K.fx, K.fy, K.cx, K.cy, K.depth_scale], np.float32),
                         iters=np.int32(iters), dist_thresh=np.float32(dist), T_wc=Twc,
                         T_rel=np.stack(rel))
@@ -107,14 +113,28 @@ def make_recording(name, n=3, W=24, H=16, seed=7):
     print(f"{name}: {n} frames, {len(b)} bytes")
 
 
+PAIR_CASES = [("pair_80x60", 80, 60, 0), ("pair_160x120", 160, 120, 1),
+              ("pair_97x53", 97, 53, 2)]
+SEQ_CASES = [("seq_128x96", 128, 96, 6)]
+
+
 def main():
+    if "--survey" in sys.argv:
+        out = os.path.join(HERE, "survey")
+        os.makedirs(out, exist_ok=True)
+        with oracle.spec("survey"):
+            for args in PAIR_CASES:
+                make_pair_case(*args, out=out)
+            for args in SEQ_CASES:
+                make_seq_case(*args, out=out)
+        return
     make_recording("rec_24x16_3f.bin")
     np.savez_compressed(os.path.join(HERE, "kat_backproject.npz"),
                         table=np.array(KAT, dtype=np.int64))
-    make_pair_case("pair_80x60", 80, 60, 0)
-    make_pair_case("pair_160x120", 160, 120, 1)
-    make_pair_case("pair_97x53", 97, 53, 2)
-    make_seq_case("seq_128x96", 128, 96, 6)
+    for args in PAIR_CASES:
+        make_pair_case(*args)
+    for args in SEQ_CASES:
+        make_seq_case(*args)
 
 
 if __name__ == "__main__":

@@ -811,3 +811,44 @@ def test_plain_c_rccl_demo_one_rank(tmp_path):
     assert not st.any()
     for p in range(n):
         assert _pose_err(T[p], T_cpu[p]) <= POSE_TOL, p
+
+
+def test_headline_512_pairs_one_launch():
+    """C4 at N = 1, exactly as bench.py's `value` runs it: 512 pairs @640x480
+    in ONE align_pairs_device call, i.e. the persistent k_icp with the
+    >256-pair work geometry (3072 chunks per iteration, 6 per pair;
+    reduce_geometry).  Every one of the 512 poses within 1e-5 of the oracle's;
+    the correspondence count of every pair at every iteration equal to the
+    oracle's (the association inside k_icp, which emits no indices, picks the
+    same pixel set) and sum r^2 within rel 1e-9; indices at the final fp32
+    pose bit-exact on pairs 0, 255, 256 and 511 (first/last pair of each half
+    of the batch, the 8-GPU shard boundaries 256 apart)."""
+    import torch
+    n, W, H = 512, 640, 480
+    src, dst, _ = youth_synth.pairs(0, n, W, H)
+    ds = torch.from_numpy(src).cuda()
+    dd = torch.from_numpy(dst).cuda()
+    out = torch.zeros((n, 16), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    with youth_icp.IcpContext(W, H, n, iters=10) as ctx:
+        ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), n, d_T_out=out.data_ptr())
+        ctx.sync()
+        assert ctx.get_plan()["kernel"].startswith("k_prep + k_icp (persistent)")
+        T64, T32, st = ctx.get_poses(n)
+        cnt, r2 = ctx.get_stats(n, 10)
+        Tout = out.cpu().numpy().reshape(n, 4, 4)
+    del ds, dd
+    T_cpu, st_cpu, stats = oracle.align_batch(src, dst, iters=10,
+                                              n_threads=min(16, os.cpu_count() or 1),
+                                              want_stats=True)
+    assert not st.any() and not st_cpu.any()
+    err = np.abs(T64[:, :3, :4] - T_cpu[:, :3, :4]).max(axis=(1, 2))
+    assert float(err.max()) <= POSE_TOL, (int(err.argmax()), float(err.max()))
+    assert np.array_equal(Tout, T32)
+    assert np.array_equal(cnt, stats[..., 0]), np.argwhere(cnt != stats[..., 0])[:4]
+    np.testing.assert_allclose(r2, stats[..., 1], rtol=1e-9)
+    K = oracle.viewer_K(W, H)
+    with youth_icp.IcpContext(W, H, 2) as ctx:
+        for p in (0, 255, 256, 511):
+            g_idx, _ = ctx.reduce(src[p], dst[p], T32[p][:3])
+            assert np.array_equal(g_idx, oracle.associate(src[p], dst[p], T32[p][:3], K)), p

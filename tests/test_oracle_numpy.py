@@ -13,6 +13,10 @@ equation sums are compared exactly too: the products are exact in float64
 and np.cumsum adds in pixel order, the oracle's summation order.
 The SE(3) exp and the 6x6 solve (a10) are cross-checked against scipy /
 numpy in test_oracle.py.
+
+Spec a7/a8 exists in two arithmetics (oracle_set_spec): the default fma
+chains, and SURVEY.md §8a a7/a8 as worded (no FMA, IEEE division), which is
+plain numpy float32 evaluated left to right (``spec="survey"`` below).
 """
 import numpy as np
 import pytest
@@ -93,45 +97,60 @@ def normals_np(X, Y, Z):
     return N
 
 
-def associate_np(S, Tg, Nt, T12, K, thr):
+def associate_np(S, Tg, Nt, T12, K, thr, spec="fma"):
     """Spec a7 for every source pixel: target index or -1, and P'."""
     sx, sy, sz = (a.ravel() for a in S)
     tX, tY, tZ = (a.ravel() for a in Tg)
     nX, nY, nZ = (a.ravel() for a in Nt)
     H, W = S[2].shape
     T = np.asarray(T12, f32).ravel()
-    qx = fma32(T[2], sz, fma32(T[1], sy, fma32(T[0], sx, T[3])))
-    qy = fma32(T[6], sz, fma32(T[5], sy, fma32(T[4], sx, T[7])))
-    qz = fma32(T[10], sz, fma32(T[9], sy, fma32(T[8], sx, T[11])))
+    if spec == "survey":
+        # SURVEY §8a a7: P' = R P + t, fixed order, no FMA;
+        # u' = floor(fx P'x / P'z + cx + 0.5), left to right, IEEE division
+        qx = ((T[0] * sx + T[1] * sy) + T[2] * sz) + T[3]
+        qy = ((T[4] * sx + T[5] * sy) + T[6] * sz) + T[7]
+        qz = ((T[8] * sx + T[9] * sy) + T[10] * sz) + T[11]
+    else:
+        qx = fma32(T[2], sz, fma32(T[1], sy, fma32(T[0], sx, T[3])))
+        qy = fma32(T[6], sz, fma32(T[5], sy, fma32(T[4], sx, T[7])))
+        qz = fma32(T[10], sz, fma32(T[9], sy, fma32(T[8], sx, T[11])))
     ok = (sz > 0) & (qz > 0)
     with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
-        rz = f32(1) / qz
-        fu = np.floor(fma32(f32(K.fx) * qx, rz, f32(K.cx) + f32(0.5)))
-        fv = np.floor(fma32(f32(K.fy) * qy, rz, f32(K.cy) + f32(0.5)))
+        if spec == "survey":
+            fu = np.floor(((f32(K.fx) * qx) / qz + f32(K.cx)) + f32(0.5))
+            fv = np.floor(((f32(K.fy) * qy) / qz + f32(K.cy)) + f32(0.5))
+        else:
+            rz = f32(1) / qz
+            fu = np.floor(fma32(f32(K.fx) * qx, rz, f32(K.cx) + f32(0.5)))
+            fv = np.floor(fma32(f32(K.fy) * qy, rz, f32(K.cy) + f32(0.5)))
     ok &= (fu >= 0) & (fu < W) & (fv >= 0) & (fv < H)
     j = np.where(ok, np.where(ok, fv, 0).astype(np.int64) * W + np.where(ok, fu, 0).astype(np.int64), 0)
     ok &= tZ[j] > 0
     ok &= ~((nX[j] == 0) & (nY[j] == 0) & (nZ[j] == 0))
     dx, dy, dz = qx - tX[j], qy - tY[j], qz - tZ[j]
-    d2 = fma32(dz, dz, fma32(dy, dy, dx * dx))
+    d2 = (dx * dx + dy * dy) + dz * dz if spec == "survey" else fma32(dz, dz, fma32(dy, dy, dx * dx))
     thr2 = f32(thr) * f32(thr)
     ok &= d2 < thr2
     return np.where(ok, j, -1).astype(np.int32), (qx, qy, qz)
 
 
-def reduce_np(S, Tg, Nt, T12, K, thr):
+def reduce_np(S, Tg, Nt, T12, K, thr, spec="fma"):
     """Spec a8-a9: r = n . (P' - P_t), J = [P' x n, n]; the 21 + 6 + 1 + 1
     sums of exact float64 products in pixel order."""
-    idx, (qx, qy, qz) = associate_np(S, Tg, Nt, T12, K, thr)
+    idx, (qx, qy, qz) = associate_np(S, Tg, Nt, T12, K, thr, spec)
     m = idx >= 0
     j = idx[m]
     tX, tY, tZ = (a.ravel()[j] for a in Tg)
     nx, ny, nz = (a.ravel()[j] for a in Nt)
     q0, q1, q2 = qx[m], qy[m], qz[m]
     dx, dy, dz = q0 - tX, q1 - tY, q2 - tZ
-    r = fma32(nz, dz, fma32(ny, dy, nx * dx))
-    J = [fma32(q1, nz, -(q2 * ny)), fma32(q2, nx, -(q0 * nz)), fma32(q0, ny, -(q1 * nx)),
-         nx, ny, nz]
+    if spec == "survey":
+        r = (nx * dx + ny * dy) + nz * dz
+        J = [q1 * nz - q2 * ny, q2 * nx - q0 * nz, q0 * ny - q1 * nx, nx, ny, nz]
+    else:
+        r = fma32(nz, dz, fma32(ny, dy, nx * dx))
+        J = [fma32(q1, nz, -(q2 * ny)), fma32(q2, nx, -(q0 * nz)), fma32(q0, ny, -(q1 * nx)),
+             nx, ny, nz]
     J64 = [a.astype(f64) for a in J]
     r64 = r.astype(f64)
     terms = [J64[a] * J64[b] for a in range(6) for b in range(a, 6)]
@@ -149,8 +168,9 @@ def _cases():
     yield "synth640_survey_noise", src[0], dst[0], oracle.viewer_K(640, 480), 0.10
 
 
+@pytest.mark.parametrize("spec", ["fma", "survey"])
 @pytest.mark.parametrize("case", list(_cases()), ids=lambda c: c[0])
-def test_numpy_restatement_equals_oracle_bitwise(case):
+def test_numpy_restatement_equals_oracle_bitwise(case, spec):
     _, src, dst, K, thr = case
     S = backproject_np(src, K)
     Tg = backproject_np(dst, K)
@@ -169,9 +189,12 @@ def test_numpy_restatement_equals_oracle_bitwise(case):
     for T in (np.eye(4)[:3], np.hstack([np.eye(3), [[0.004], [-0.002], [0.003]]]),
               np.hstack([R, [[0.04], [0.01], [-0.02]]])):
         T12 = T.astype(f32)
-        neq, idx = reduce_np(S, Tg, Nt, T12, K, thr)
-        assert np.array_equal(idx, oracle.associate(src, dst, T12, K, thr).ravel())
-        assert np.array_equal(neq.view(np.uint64), oracle.reduce(src, dst, T12, K, thr).view(np.uint64))
+        neq, idx = reduce_np(S, Tg, Nt, T12, K, thr, spec)
+        with oracle.spec(spec):
+            o_idx = oracle.associate(src, dst, T12, K, thr).ravel()
+            o_neq = oracle.reduce(src, dst, T12, K, thr)
+        assert np.array_equal(idx, o_idx)
+        assert np.array_equal(neq.view(np.uint64), o_neq.view(np.uint64))
         assert neq[28] > 0
 
 
