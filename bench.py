@@ -87,9 +87,24 @@ def parse():
                     help="skip the viewer point-list leg (SURVEY §8 f4; rank 0, N=1)")
     ap.add_argument("--no-host-io", action="store_true",
                     help="skip the PCIe-inclusive host-buffer API leg (rank 0, N=1)")
+    ap.add_argument("--spec", choices=["survey", "fma"],
+                    default=os.environ.get("YOUTH_ICP_SPEC", "survey"),
+                    help="arithmetic of spec a7/a8 (youth_icp_set_spec): survey = SURVEY.md §8a "
+                         "as worded (the default), fma = the opt-in fma-chain form; the oracle "
+                         "checks in the same spec")
+    ap.add_argument("--no-spec-parity", action="store_true",
+                    help="skip the spec-parity leg (rank 0, N=1)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes and VALU figures of k_icp (tools/pmc_traffic.py)")
     return ap.parse_args()
+
+
+def oracle_mod():
+    """The C oracle (the checker; legs after the timed region), in the spec
+    the library runs (YOUTH_ICP_SPEC, set from --spec in main)."""
+    import oracle
+    oracle.set_spec(os.environ.get("YOUTH_ICP_SPEC", "survey"))
+    return oracle
 
 
 def kernel_digest():
@@ -339,6 +354,15 @@ def run_pairs(R):
     result["sched_last_step"] = {"epoch_polls": spins, "items_waited": waited}
     result["kernel_path"] = ctx.get_plan()
     result["status_nonzero"] = int((st_gpu != 0).sum())
+    # every rank's own k_icp / k_prep / gather times and the group's size
+    # (collective: all ranks), so an N > 1 line shows that N ranks ran and
+    # splits compute from the collective
+    gms = gather_ms(R, poses[0], gathered[0], world, counts, main, side)
+    result["ranks"] = youth_dist.rank_report({
+        "k_icp_ms": result["kernel_ms_per_step"]["k_icp"],
+        "k_prep_ms": result["kernel_ms_per_step"]["k_prep"],
+        "gather_ms": gms if gms is not None else 0.0}, world)
+    result["ranks"]["gather_timed"] = gms is not None
     if rank == 0 and world == 1:
         leg = {}
         if not a.no_cpu_baseline:
@@ -355,9 +379,103 @@ def run_pairs(R):
             leg["c5"] = c5_rate(R, F=a.c5_frames, stream_frames=min(300, a.c5_frames))
         if not a.no_viewer:
             leg["viewer_cloud"] = viewer_cloud_rate(R, d_dst[:64], dst[:64])
+        if not a.no_spec_parity:
+            leg["spec_parity"] = spec_parity(a, main)
+            leg["spec_parity"]["other_spec_rate"] = other_spec_rate(R, ctx, step, n_glob)
         result.update(leg)
     ctx.close()
     return result
+
+
+def gather_ms(R, local, out, world, counts, main, side, reps=5):
+    """Median time of the pose all-gather alone (after the timed region, the
+    align idle): HIP events on the launch stream before the collective and
+    on the side stream after its wait.  None without a process group."""
+    if not R.dist_on:
+        return None
+    ts = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(main)
+        work = youth_dist.gather_poses_ragged_async(local, out, world, counts)
+        with torch.cuda.stream(side):
+            if work is not None:
+                work.wait()
+            else:
+                side.wait_stream(main)
+            e1.record(side)
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    return float(np.median(ts))
+
+
+def other_spec_rate(R, ctx, step, n_glob):
+    """The headline step in the OTHER spec a7/a8 arithmetic on the same
+    context and inputs (after the timed region): its rate and k_icp time."""
+    a = R.a
+    other = "fma" if a.spec == "survey" else "survey"
+    ctx.spec = other
+    for _ in range(5):
+        step()
+    ctx.set_timing(True, iteration_kernel_only=True)
+    el = R.window(step, a.steps)
+    ms, n = ctx.get_timing(0)
+    ctx.set_timing(False)
+    ctx.spec = a.spec
+    return {"spec": other, "value": n_glob * a.steps / el, "unit": "aligns/s",
+            "k_icp_ms": ms / max(n, 1)}
+
+
+def spec_parity(a, main):
+    """how far the GPU's poses sit from SURVEY §8a's
+    literal arithmetic (the survey-spec oracle) in each spec the kernels
+    implement, on C2's 640x480 pairs (64), C3 (2 pairs at 1280x960, 20
+    iterations), C5 (a 201-frame sequence: 200 relative poses) and at SURVEY
+    §8d's noise (16 pairs).  Also each spec against the oracle in the same
+    spec (the bit-exactness bar, ~1e-13)."""
+    oracle = oracle_mod()
+    cases = {}
+    s64 = youth_synth.pairs(0, 64)
+    cases["c2_64_pairs"] = (s64[0], s64[1], 640, 480, 10, None)
+    s3 = youth_synth.pairs(0, 2, 1280, 960)
+    cases["c3_2_pairs_1280x960_20it"] = (s3[0], s3[1], 1280, 960, 20, None)
+    fr, _ = youth_synth.sequence(0, 201)
+    cases["c5_200_pairs"] = (fr[1:], fr[:-1], 640, 480, 10, fr)
+    sn = youth_synth.pairs(0, 16, flags=youth_synth.SURVEY_FLAGS)
+    cases["survey_noise_16_pairs"] = (sn[0], sn[1], 640, 480, 10, None)
+    out = {}
+    worst = {}
+    for name, (src, dst, W, H, iters, frames) in cases.items():
+        n = src.shape[0]
+        K = youth_icp.default_intrinsics(W, H)
+        row = {"pairs": n}
+        ref = {}
+        for sp in ("survey", "fma"):
+            with oracle.spec(sp):
+                ref[sp], _ = oracle.align_batch(src, dst, K=oracle.viewer_K(W, H), iters=iters,
+                                                n_threads=min(n, _cpus()))
+        ctx = youth_icp.IcpContext(W, H, max(n, 2), K=K, iters=iters)
+        if frames is not None:
+            df = torch.from_numpy(frames).cuda()
+        else:
+            ds, dd = torch.from_numpy(src).cuda(), torch.from_numpy(dst).cuda()
+        for sp in ("survey", "fma"):
+            ctx.spec = sp
+            if frames is not None:
+                ctx.align_sequence_device(df.data_ptr(), n + 1, stream=main.cuda_stream)
+            else:
+                ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), n, stream=main.cuda_stream)
+            T, _, st = ctx.get_poses(n)
+            row[f"gpu_{sp}_vs_survey_oracle"] = pose_err(T, ref["survey"])
+            row[f"gpu_{sp}_vs_{sp}_oracle"] = pose_err(T, ref[sp])
+            row[f"gpu_{sp}_status_nonzero"] = int((st != 0).sum())
+            worst[sp] = max(worst.get(sp, 0.0), row[f"gpu_{sp}_vs_survey_oracle"])
+        ctx.close()
+        out[name] = row
+    out["max_vs_survey_oracle"] = worst
+    out["default_within_tol_of_survey_spec"] = bool(worst[a.spec] <= POSE_TOL)
+    return out
 
 
 def single_pair_rate(R, d_src, d_dst, src0, dst0, steps=400, warmup=40):
@@ -365,7 +483,7 @@ def single_pair_rate(R, d_src, d_dst, src0, dst0, steps=400, warmup=40):
     to back on the caller's (torch) stream: the latency path of
     processSlamFrame's tracker, inputs resident in HBM; pose checked against
     the C oracle's pose of the same pair."""
-    import oracle
+    oracle = oracle_mod()
     a = R.a
     ctx = youth_icp.IcpContext(a.width, a.height, 2, iters=a.iters, device=R.local)
     out = torch.zeros((1, 16), dtype=torch.float32, device="cuda")
@@ -395,7 +513,7 @@ def c3_rate(R, n=16, W=1280, H=960, iters=20):
     iterations, 1 GPU: one pair per call (the LDS-tiled small-batch kernel)
     and an n-pair batch per call (persistent kernel); every pose checked
     against the C oracle (OpenMP over the 16 pairs)."""
-    import oracle
+    oracle = oracle_mod()
     src, dst, _ = youth_synth.pairs(0, n, W, H)
     d_src, d_dst = torch.from_numpy(src).cuda(), torch.from_numpy(dst).cuda()
     stream = torch.cuda.current_stream().cuda_stream
@@ -414,9 +532,33 @@ def c3_rate(R, n=16, W=1280, H=960, iters=20):
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         T, _, st = ctx.get_poses(k)
+        plan = ctx.get_plan()
+        # roofline of the iteration kernel: its own
+        # 18 B per pixel-iteration x W x H x iters x pairs per launch over the
+        # launch time (HIP events on the launch stream, a separate pass)
+        ctx.set_timing(True, iteration_kernel_only=True)
+        for _ in range(min(reps, 20)):
+            ctx.align_pairs_device(d_src.data_ptr(), d_dst.data_ptr(), k,
+                                   d_T_out=out.data_ptr(), stream=stream)
+        torch.cuda.synchronize()
+        ms, nl = ctx.get_timing(0)
+        ctx.set_timing(False)
+        avg = ms / max(nl, 1)
+        alg = ICP_BYTES_PER_PX_ITER * W * H * iters * k
+        ach = alg / (avg * 1e-3) / 1e9
+        kname = plan["kernel"]
         res[tag] = {"value": k * reps / el, "unit": "aligns/s", "pairs_per_call": k,
-                    "us_per_call": el / reps * 1e6, "kernel_path": ctx.get_plan(),
-                    "status_nonzero": int((st != 0).sum())}
+                    "us_per_call": el / reps * 1e6, "kernel_path": plan,
+                    "status_nonzero": int((st != 0).sum()),
+                    "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS,
+                                 "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+                                 "kernel": ("k_icp_coop (target prep fused: its 18 B/px "
+                                            "not counted)") if kname == "k_icp_coop" else
+                                           "k_icp (persistent; k_prep separate)",
+                                 "algorithmic_bytes_per_launch": alg,
+                                 "algorithmic_model": "18 B per pixel-iteration x W x H x "
+                                                      "iters x pairs",
+                                 "avg_launch_ms": avg, "launches": nl}}
         res[tag]["_T"] = T
     threads = min(n, _cpus())
     t0 = time.perf_counter()
@@ -439,7 +581,7 @@ def c5_rate(R, F=1000, sample_every=16, stream_frames=300, reps=3):
     per call, and streamed frame by frame from host memory through the
     tracker (processSlamFrame's path).  Relative poses checked against the C
     oracle on every `sample_every`-th pair; streamed poses against the batch's."""
-    import oracle
+    oracle = oracle_mod()
     a = R.a
     W, H = a.width, a.height
     frames, _ = youth_synth.sequence(0, F, W, H)
@@ -535,7 +677,7 @@ def survey_noise_parity(a, ctx, main, n=16):
     """Parity on SURVEY §8d's noise level (sigma = 1.5 mm Z^2; the bench's
     default synthetic pairs use 0.25 mm Z^2): n pairs through the
     same context vs the C oracle."""
-    import oracle
+    oracle = oracle_mod()
     src, dst, _ = youth_synth.pairs(0, n, a.width, a.height, flags=youth_synth.SURVEY_FLAGS)
     ds, dd = torch.from_numpy(src).cuda(), torch.from_numpy(dst).cuda()
     ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), n, stream=main.cuda_stream)
@@ -586,7 +728,7 @@ def viewer_cloud_rate(R, d_depth, depth_host, reps=20, warmup=3):
                         "algorithmic_bytes_per_call": nbytes,
                         "kernels": "k_cloud_count + k_cloud_scan + k_cloud_emit"}}
     if not a.no_cpu_baseline:
-        import oracle
+        oracle = oracle_mod()
         want = oracle.viewer_cloud(depth_host[0], rgb[0])
         got = verts[0, : int(cnt[0])].cpu().numpy()
         res["bit_exact_vs_cpu"] = bool(got.shape == want.shape and
@@ -634,6 +776,21 @@ def run_sequence(R):
     }
     result["window_rates"] = [(F - 1) * a.steps / s for s in spread]
     result["roofline"] = roofline_icp(a, kt, max(npairs, 1), W, H)
+    g_ms = None
+    if R.dist_on:
+        ts = []
+        for _ in range(5):
+            R.barrier_sync()
+            t0 = time.perf_counter()
+            youth_dist.gather_ragged(rel[:npairs], world, max_rows, counts)
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t0) * 1e3)
+        g_ms = float(np.median(ts))
+    result["ranks"] = youth_dist.rank_report({
+        "k_icp_ms": kt["k_icp"][0] / max(kt["k_icp"][1], 1),
+        "k_prep_ms": kt["k_prep"][0] / max(kt["prep_pass_steps"], 1),
+        "gather_ms": g_ms if g_ms is not None else 0.0}, world)
+    result["ranks"]["gather_timed"] = g_ms is not None
     if rank == 0:
         T = youth_dist.compose_trajectory(traj["T"].cpu().numpy().reshape(-1, 4, 4))
         result["trajectory_frames"] = int(T.shape[0])
@@ -657,6 +814,10 @@ def base_result(R, value, elapsed):
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "fp32",
+        "spec": {"name": a.spec,
+                 "a7_a8": ("SURVEY.md §8a as worded: no FMA, IEEE division fx P'x / P'z"
+                           if a.spec == "survey" else
+                           "fma chains, one correctly rounded reciprocal (opt-in)")},
         "data": "synthetic (ray-cast room scene, int16 mm depth, seeds 0x5EED0000+pair / "
                 "0x5EED1000 sequence)",
     }
@@ -693,7 +854,7 @@ def cpu_baseline(a, src, dst, T_gpu):
     on the GPU pool) and (ii) on min(pairs, visible CPUs) threads; the faster
     is the reported value.  Plus (iii) one thread on a 2-pair sample, and the
     SE(3) error of the GPU poses on every sampled pair."""
-    import oracle
+    oracle = oracle_mod()
 
     cpus = _cpus()
     S = src.shape[0]
@@ -741,6 +902,7 @@ def cpu_baseline(a, src, dst, T_gpu):
 
 def main():
     a = parse()
+    os.environ["YOUTH_ICP_SPEC"] = a.spec   # every context of this run (youth_icp_create)
     R = Run(a)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))   # the checker (legs after timing)
     # a non-default torch stream: its handle is what every align is issued on,

@@ -42,7 +42,12 @@ youth_dist* youth_dist_create(int nranks, int rank, int device,
  * d_all: DEVICE [n_pairs][16] fp32, receives all rows in pair order (may not
  * overlap d_local).  Enqueued on `stream` (hipStream_t as void*, NULL = the
  * default stream) and asynchronous, like any RCCL collective: every rank
- * must call it with the same n_pairs, in the same order. */
+ * must call it with the same n_pairs, in the same order.  Calls of one
+ * communicator share its scratch rows, so they are ordered across streams:
+ * a call from a stream other than the previous call's first waits for all
+ * work enqueued on that previous stream (one event, only at a switch), so
+ * double-buffered callers on two streams never mix batches.  Not
+ * thread-safe: one host thread per communicator. */
 int youth_dist_allgather_poses(youth_dist* d, const float* d_local, int n_pairs, float* d_all,
                                void* stream);
 

@@ -132,10 +132,13 @@ int youth_icp_device_count(void);
 int youth_icp_fastdiv_enabled(youth_icp_ctx* ctx);
 
 /* Arithmetic of spec a7/a8 (association, residual, Jacobian):
- *   YOUTH_SPEC_FMA    fma chains and one correctly rounded reciprocal 1/P'z;
- *   YOUTH_SPEC_SURVEY SURVEY.md §8a a7/a8 + §7 word for word: products and
- *                     sums rounded separately in a fixed order (no FMA), the
- *                     projection quotient fx P'x / P'z an IEEE division.
+ *   YOUTH_SPEC_SURVEY (default) SURVEY.md §8a a7/a8 + §7 word for word:
+ *                     products and sums rounded separately in a fixed order
+ *                     (no FMA), the projection quotient fx P'x / P'z an IEEE
+ *                     division;
+ *   YOUTH_SPEC_FMA    opt-in: fma chains and one correctly rounded
+ *                     reciprocal 1/P'z (~6 % faster k_icp; poses move by up
+ *                     to ~1e-5 against the survey spec).
  * Both are bit-exact (indices) against the oracle run in the same spec
  * (oracle_set_spec).  youth_icp_set_spec selects one for the context's later
  * aligns and returns the previous spec (EINVAL for another value); the
@@ -197,7 +200,15 @@ void youth_icp_destroy(youth_icp_ctx* ctx);
  * returns after enqueueing; use youth_icp_sync / youth_icp_get_poses.  One
  * context's aligns must execute in order (one stream, or ordered by the
  * caller): they share its workspace and per-call hand-off state.  Small
- * batches run as one cooperative launch (youth_icp_get_plan). */
+ * batches run as one cooperative launch (youth_icp_get_plan): its
+ * workgroups wait on each other, so the whole grid must be co-resident.  It
+ * is launched as a plain kernel sized to an idle device, with every such
+ * launch of the process ordered per device; that assumes this process owns
+ * the GPU (no other process's kernels holding CUs meanwhile).  On a shared
+ * GPU set YOUTH_ICP_COOP_LAUNCH=runtime (hipLaunchCooperativeKernel: the
+ * runtime admits the grid or refuses it, and a refusal falls back to the
+ * persistent kernel) or YOUTH_ICP_NO_COOP=1; a grid that is not co-resident
+ * ends at the spin bound with YOUTH_STATUS_TIMEOUT, never a hang. */
 int youth_icp_align_pairs_device(youth_icp_ctx* ctx, const int16_t* d_src,
                                  const int16_t* d_dst, int n_pairs,
                                  const double* T_init, float* d_T_out,

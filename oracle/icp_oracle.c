@@ -78,13 +78,14 @@ void oracle_normals(const float* X, const float* Y, const float* Z, int W, int H
 }
 
 /* Which restatement of spec a7/a8 the association and residual follow
- * (oracle_set_spec): ORACLE_SPEC_FMA, the build's default (fma
- * chains, one correctly rounded reciprocal), or ORACLE_SPEC_SURVEY, SURVEY.md
- * §8a a7/a8 and §7 word for word: separately rounded products and sums in a
- * fixed order, no FMA, and the projection's quotient as an IEEE division,
- * u' = floor(fx P'x / P'z + cx + 0.5) evaluated left to right.  Set before
- * a run; read-only while one is in flight (OpenMP threads only read it). */
-static int g_spec = ORACLE_SPEC_FMA;
+ * (oracle_set_spec): ORACLE_SPEC_SURVEY, the default, is SURVEY.md §8a a7/a8
+ * and §7 word for word: separately rounded products and sums in a fixed
+ * order, no FMA, and the projection's quotient as an IEEE division, u' =
+ * floor(fx P'x / P'z + cx + 0.5) evaluated left to right; ORACLE_SPEC_FMA is
+ * the opt-in fma-chain form (one correctly rounded reciprocal).
+ * Set before a run; read-only while one is in flight (OpenMP threads only
+ * read it). */
+static int g_spec = ORACLE_SPEC_SURVEY;
 
 int oracle_set_spec(int spec)
 {

@@ -44,12 +44,12 @@ typedef struct oracle_intrinsics {
 #define ORACLE_NEQ 29
 
 /* Arithmetic of spec a7/a8 (association, residual, Jacobian):
- *   ORACLE_SPEC_FMA    DESIGN.md §2, what the kernels run by default: fma
- *                      chains and one correctly rounded reciprocal 1/P'z;
- *   ORACLE_SPEC_SURVEY SURVEY.md §8a a7/a8 + §7 literally: no FMA (products
- *                      and sums rounded separately, fixed order) and IEEE
- *                      division fx P'x / P'z (youth_icp_set_spec's
- *                      YOUTH_SPEC_SURVEY on the GPU).
+ *   ORACLE_SPEC_SURVEY (default) SURVEY.md §8a a7/a8 + §7 literally: no FMA
+ *                      (products and sums rounded separately, fixed order)
+ *                      and IEEE division fx P'x / P'z — what the kernels run
+ *                      by default (YOUTH_SPEC_SURVEY);
+ *   ORACLE_SPEC_FMA    the opt-in fma form: fma chains and one
+ *                      correctly rounded reciprocal 1/P'z (YOUTH_SPEC_FMA).
  * Back-projection, normals, reduction, solve and update are common.
  * oracle_set_spec returns the previous spec (-1: unknown spec). */
 #define ORACLE_SPEC_FMA 0

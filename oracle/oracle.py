@@ -67,8 +67,8 @@ def load_library() -> ctypes.CDLL:
     return lib
 
 
-SPEC_FMA = 0      # ORACLE_SPEC_FMA: DESIGN.md §2 (the kernels' default)
-SPEC_SURVEY = 1   # ORACLE_SPEC_SURVEY: SURVEY.md §8a a7/a8 + §7 literally
+SPEC_FMA = 0      # ORACLE_SPEC_FMA: DESIGN.md §2's opt-in fma form
+SPEC_SURVEY = 1   # ORACLE_SPEC_SURVEY (default): SURVEY.md §8a a7/a8 + §7 literally
 SPECS = {"fma": SPEC_FMA, "survey": SPEC_SURVEY}
 
 

@@ -24,6 +24,14 @@ struct youth_dist {
     float* staging = nullptr;  // host variant: [max_count + n_pairs][16]
     size_t staging_rows = 0;
     hipStream_t stream = nullptr;  // host variant's stream
+    // every gather stages through `scratch`: calls are ordered across streams
+    // (the first call from a stream other than the previous call's waits for
+    // everything enqueued on that previous stream so far, its gather
+    // included), so double-buffering callers on two streams cannot mix
+    // batches in the scratch rows
+    hipStream_t last = nullptr;
+    bool any = false;
+    hipEvent_t order = nullptr;
 };
 
 static thread_local std::string g_err;
@@ -122,6 +130,18 @@ int youth_dist_allgather_poses(youth_dist* d, const float* d_local, int n_pairs,
     if (count > 0 && !d_local) return fail(YOUTH_EINVAL, "allgather_poses: null d_local");
     if (hipSetDevice(d->device) != hipSuccess) return fail(YOUTH_EHIP, "hipSetDevice");
     const hipStream_t s = (hipStream_t)stream;
+    if (d->any && d->last != s) {
+        // stream switch: mark the previous stream's work now and wait for it
+        // (a stream the caller destroyed since is rejected by the runtime:
+        // its work was released with it)
+        if (!d->order && hipEventCreateWithFlags(&d->order, hipEventDisableTiming) != hipSuccess)
+            return fail(YOUTH_EHIP, "hipEventCreate");
+        if (hipEventRecord(d->order, d->last) != hipSuccess) (void)hipGetLastError();
+        else if (hipStreamWaitEvent(s, d->order, 0) != hipSuccess)
+            return fail(YOUTH_EHIP, "hipStreamWaitEvent");
+    }
+    d->last = s;
+    d->any = true;
     const size_t rows = (size_t)d->nranks * max_count;
     if (rows > d->scratch_rows) {
         // a previous gather may still read the old scratch on some stream
@@ -205,6 +225,8 @@ void youth_dist_destroy(youth_dist* d)
     (void)hipSetDevice(d->device);
     if (d->stream) (void)hipStreamSynchronize(d->stream);
     if (d->comm) (void)ncclCommDestroy(d->comm);
+    if (d->any && d->last) (void)hipStreamSynchronize(d->last);
+    if (d->order) (void)hipEventDestroy(d->order);
     if (d->scratch) (void)hipFree(d->scratch);
     if (d->staging) (void)hipFree(d->staging);
     if (d->stream) (void)hipStreamDestroy(d->stream);

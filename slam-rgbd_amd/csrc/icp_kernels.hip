@@ -170,10 +170,10 @@ __device__ __forceinline__ float proj_rcp_rn(float den)
 }
 
 // Which arithmetic spec a7/a8 runs in (youth_icp_set_spec):
-//   kSpecFma    fma chains and one correctly rounded reciprocal 1/P'z;
-//   kSpecSurvey SURVEY.md §8a a7/a8 + §7 literally: separately rounded
-//               products and sums in a fixed order (no FMA) and the
-//               projection quotient fx P'x / P'z as an IEEE division.
+//   kSpecSurvey (default) SURVEY.md §8a a7/a8 + §7 literally: separately
+//               rounded products and sums in a fixed order (no FMA) and the
+//               projection quotient fx P'x / P'z as an IEEE division;
+//   kSpecFma    opt-in: fma chains and one correctly rounded reciprocal.
 // The oracle restates both (oracle_set_spec); every kernel of the iteration
 // (k_icp, k_icp_coop, k_reduce) is instantiated for each.
 constexpr int kSpecFma = YOUTH_SPEC_FMA;
@@ -586,17 +586,17 @@ struct InitArgs {
     unsigned* head_err;
 };
 
-__device__ __forceinline__ void init_pairs(const InitArgs& ia)
+__device__ __forceinline__ void init_pairs(const InitArgs& ia, int tx, int ty, int f, int n_frames)
 {
-    if (blockIdx.x != 0 || blockIdx.y != 0) return;
-    if (blockIdx.z == 0 && threadIdx.x == 0 && ia.head_err) {
+    if (tx != 0 || ty != 0) return;
+    if (f == 0 && threadIdx.x == 0 && ia.head_err) {
         ia.head_err[kQHead] = 0u;
         ia.head_err[kQError] = 0u;
         ia.head_err[kQSpins] = 0u;
         ia.head_err[kQWaited] = 0u;
     }
     const int t = threadIdx.x;
-    for (int p = blockIdx.z; p < ia.n; p += gridDim.z) {
+    for (int p = f; p < ia.n; p += n_frames) {
         if (t < 16) {
             const double v = ia.T_init ? ia.T_init[(size_t)p * 16 + t] : ((t % 5) == 0 ? 1.0 : 0.0);
             ia.T64[(size_t)p * 16 + t] = v;
@@ -611,22 +611,44 @@ __device__ __forceinline__ void init_pairs(const InitArgs& ia)
     }
 }
 
+// One workgroup per 64 x 48 tile; a 1-D grid of tiles_x x tiles_y x n_frames
+// workgroups.  xcd_map = 1: workgroups are dealt round-robin over the 8 XCDs
+// (b and b + 8 share one; MI355X_MICROARCH.md "Workgroup dispatch"), so
+// workgroup b takes tile t = (its XCD's share start) + b / 8: each XCD walks
+// ONE contiguous run of tiles (frame-major, row-major within a frame), and a
+// tile's horizontal and vertical halo lines belong to tiles that the same
+// XCD processes at about the same time, i.e. are hits in that XCD's L2
+// instead of fetches of lines that neighbouring tiles on other XCDs own.
+// xcd_map = 0: t = b (row-major over the frames: neighbours on other XCDs).
+__device__ __forceinline__ int xcd_tile(int b, int total)
+{
+    const int q = total >> 3, r = total & 7, x = b & 7, j = b >> 3;
+    return x < r ? x * (q + 1) + j : r * (q + 1) + (x - r) * q + j;
+}
+
 template <bool kFast, bool kWide>
 __global__ __launch_bounds__(kPrepThreads) void k_prep(const int16_t* __restrict__ depth, int out0,
                                                       int W, int H, size_t P, Intr K, FastK F,
                                                       float4* __restrict__ recs,
-                                                      float* __restrict__ xyz, InitArgs ia)
+                                                      float* __restrict__ xyz, InitArgs ia,
+                                                      int tiles_x, int tiles_y, int n_frames,
+                                                      int xcd_map)
 {
-    init_pairs(ia);
+    const int total = tiles_x * tiles_y * n_frames;
+    const int t = xcd_map ? xcd_tile((int)blockIdx.x, total) : (int)blockIdx.x;
+    const int per = tiles_x * tiles_y;
+    const int f = t / per;
+    const int r = t - f * per;
+    const int ty = r / tiles_x;
+    const int tx = r - ty * tiles_x;
+    init_pairs(ia, tx, ty, f, n_frames);
     __shared__ float sX[kLdsH * kLdsW];
     __shared__ float sY[kLdsH * kLdsW];
     __shared__ float sZ[kLdsH * kLdsW];
-    const int f = blockIdx.z;
     const size_t N = (size_t)W * (size_t)H;
     prep_tile<kFast, kWide, false, kPrepThreads, kTileH>(
         depth + (size_t)f * N, recs + (size_t)(out0 + f) * P, W, H, P, K, F,
-        xyz ? xyz + (size_t)(out0 + f) * 3 * P : nullptr, blockIdx.x * kTileW, blockIdx.y * kTileH,
-        sX, sY, sZ);
+        xyz ? xyz + (size_t)(out0 + f) * 3 * P : nullptr, tx * kTileW, ty * kTileH, sX, sY, sZ);
 }
 
 // ----------------------------------------------------------------- k_solve --
@@ -2096,7 +2118,7 @@ struct youth_icp_ctx {
     Intr K{};
     FastK F{};
     bool fast = false;  // verified 2-op back-projection division
-    int spec = kSpecFma;  // spec a7/a8 arithmetic (youth_icp_set_spec, YOUTH_ICP_SPEC)
+    int spec = kSpecSurvey;  // spec a7/a8 arithmetic (youth_icp_set_spec, YOUTH_ICP_SPEC)
     youth_icp_params prm{};
     hipStream_t stream = nullptr;
 
@@ -2144,6 +2166,7 @@ struct youth_icp_ctx {
     int track_ref = -1;  // ring slot (0/1) of the tracker's reference frame
     double* coop_res_host = nullptr;  // set around a tracker align: k_icp_coop writes its result there
     bool coop_tile_src = true;        // YOUTH_ICP_COOP_TILE_SRC=0: contiguous source chunks
+    int prep_xcd_map = 0;             // YOUTH_ICP_PREP_XCD_MAP=1: k_prep tiles contiguous per XCD (slower)
     // pipelined tracking (youth_icp_track_submit / _collect): up to
     // kTrackDepth frames in flight, each with a pinned staging buffer, pinned
     // results and events
@@ -2285,7 +2308,9 @@ static int launch_prep(youth_icp_ctx* c, hipStream_t s, const int16_t* depth, in
         int rc = ensure_xyz(c);
         if (rc) return rc;
     }
-    dim3 grid((c->W + kTileW - 1) / kTileW, (c->H + kTileH - 1) / kTileH, n_frames);
+    const int tiles_x = (c->W + kTileW - 1) / kTileW, tiles_y = (c->H + kTileH - 1) / kTileH;
+    const long long blocks = (long long)tiles_x * tiles_y * n_frames;
+    if (blocks > 0x7fffffffLL) return set_error(YOUTH_EINVAL, "launch_prep: %lld tiles", blocks);
     EventPair ep{};
     int rc = ev_begin(c, s, &ep, 2);
     if (rc) return rc;
@@ -2294,8 +2319,9 @@ static int launch_prep(youth_icp_ctx* c, hipStream_t s, const int16_t* depth, in
     auto kern = c->fast ? (wide ? k_prep<true, true> : k_prep<true, false>)
                         : (wide ? k_prep<false, true> : k_prep<false, false>);
     const InitArgs ia = init ? *init : InitArgs{};
-    hipLaunchKernelGGL(kern, grid, dim3(kPrepThreads), 0, s, depth, out0, c->W, c->H, c->P, c->K,
-                       c->F, c->d_rec, xyz, ia);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kPrepThreads), 0, s, depth, out0, c->W,
+                       c->H, c->P, c->K, c->F, c->d_rec, xyz, ia, tiles_x, tiles_y, n_frames,
+                       c->prep_xcd_map);
     HIP_TRY(hipGetLastError());
     return ev_end(c, s, &ep);
 }
@@ -2776,6 +2802,17 @@ void youth_icp_destroy(youth_icp_ctx* c)
                     c->d_coop,  c->d_status_out};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
+    if (c->device >= 0 && c->device < 64) {
+        // the device's coop ordering must not take a later stream that reuses
+        // this handle for the same stream (its work is complete: synchronised
+        // above, and every earlier coop launch ran before it)
+        CoopOrder& o = g_coop_order[c->device];
+        std::lock_guard<std::mutex> lk(o.mu);
+        if (o.any && o.last == c->stream) {
+            o.any = false;
+            o.last = nullptr;
+        }
+    }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->xfer) (void)hipStreamDestroy(c->xfer);
     delete c;
@@ -2888,6 +2925,8 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         // persistent fallback of run_iterations
         const char* crf = getenv("YOUTH_ICP_TEST_REFUSE_COOP");
         c->coop_refuse = crf && *crf && *crf != '0';
+        const char* pxm = getenv("YOUTH_ICP_PREP_XCD_MAP");
+        if (pxm && *pxm == '1') c->prep_xcd_map = 1;
         const char* cts = getenv("YOUTH_ICP_COOP_TILE_SRC");
         if (cts && *cts == '0') c->coop_tile_src = false;
         const char* cmp = getenv("YOUTH_ICP_COOP_MAX_PAIRS");

@@ -225,6 +225,10 @@ void worker_main(int device)
         }
         if (!record || g_reset.load()) return;
         std::lock_guard<std::mutex> lk(g_slam_mu);
+        // resetSlam raises g_reset under this lock before it clears the
+        // trajectory: a frame of the old sequence that passed the check
+        // above sees the flag here and is not taken as the new origin
+        if (g_reset.load()) return;
         if (!has_ref || g_traj.empty()) {
             // new sequence: this frame is the world origin
             double I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
@@ -470,11 +474,14 @@ void resetSlam(void)
 {
     if (!g_running.load()) return;
     {
+        // the flag first, under the trajectory lock: finish_one re-checks it
+        // under the same lock, so no pre-reset frame is recorded after the
+        // clear
         std::lock_guard<std::mutex> lk(g_slam_mu);
+        g_reset.store(true);
         g_traj.clear();
         g_last_points = 0;
     }
-    g_reset.store(true);
     fprintf(stderr, "youth_icp: SLAM system reset\n");
 }
 

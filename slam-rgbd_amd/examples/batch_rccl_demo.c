@@ -5,7 +5,11 @@
  * all-gathered over RCCL (youth_dist.h), so every rank ends up with all of
  * them.  Rank 0 creates the communicator id and publishes it through a file
  * (written then renamed, so readers never see a partial id); the other ranks
- * wait for the file.
+ * wait for the file.  A stale id file of an earlier run is never joined:
+ * rank 0 removes it before anything else, and a reader accepts only a file
+ * written at most 30 s before the reader itself started (the ranks of one
+ * launch start together).  A rank whose align fails still joins the gather
+ * (its rows NaN) so no peer blocks in the collective, then exits 6.
  *
  * usage: batch_rccl_demo <nranks> <rank> <id_file> <n_pairs> <out.f32> [W H]
  *   e.g. one shell per GPU:  batch_rccl_demo 8 $r /tmp/youth.id 512 /tmp/T$r.f32
@@ -16,16 +20,20 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <math.h>
+#include <sys/stat.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "youth_dist.h"
 #include "youth_icp.h"
 #include "youth_synth.h"
 
-static int read_id(const char* path, unsigned char* id)
+static int read_id(const char* path, unsigned char* id, time_t started)
 {
     for (int k = 0; k < 6000; ++k) {  /* up to 60 s */
-        FILE* f = fopen(path, "rb");
+        struct stat sb;
+        FILE* f = (stat(path, &sb) == 0 && sb.st_mtime + 30 >= started) ? fopen(path, "rb") : NULL;
         if (f) {
             const size_t n = fread(id, 1, YOUTH_DIST_ID_BYTES, f);
             fclose(f);
@@ -45,6 +53,8 @@ int main(int argc, char** argv)
     }
     const int nranks = atoi(argv[1]), rank = atoi(argv[2]), n = atoi(argv[4]);
     const char* id_file = argv[3];
+    const time_t started = time(NULL);
+    if (atoi(argv[2]) == 0) (void)unlink(id_file);  /* never a stale id */
     const int W = argc > 7 ? atoi(argv[6]) : 640, H = argc > 7 ? atoi(argv[7]) : 480;
     if (nranks < 1 || rank < 0 || rank >= nranks || n < 1) return 2;
     const int ndev = youth_icp_device_count();
@@ -64,7 +74,7 @@ int main(int argc, char** argv)
             fprintf(stderr, "rank 0: cannot publish the id: %s\n", youth_dist_last_error());
             return 4;
         }
-    } else if (read_id(id_file, id) != 0) {
+    } else if (read_id(id_file, id, started) != 0) {
         fprintf(stderr, "rank %d: no id in %s\n", rank, id_file);
         return 4;
     }
@@ -83,20 +93,26 @@ int main(int argc, char** argv)
     int32_t* st = (int32_t*)malloc((size_t)(count ? count : 1) * sizeof(int32_t));
     float* all = (float*)malloc((size_t)n * 16 * sizeof(float));
     if (!src || !dst || !T || !st || !all) return 2;
-    int bad = 0;
+    int bad = 0, align_failed = 0;
     if (count > 0) {
         youth_synth_pairs(YOUTH_SYNTH_PAIR_SEED, first, count, W, H, &K,
                           YOUTH_SYNTH_NOISE | YOUTH_SYNTH_HOLES, src, dst, NULL);
         if (youth_icp_align_batch_multi(src, dst, count, W, H, &K, 10, &device, 1, T, st) !=
             YOUTH_OK) {
+            /* still join the collective (every peer is in it): NaN rows */
             fprintf(stderr, "rank %d: align: %s\n", rank, youth_icp_last_error());
-            return 6;
+            align_failed = 1;
+            for (size_t i = 0; i < (size_t)count * 16; ++i) T[i] = NAN;
         }
-        for (int p = 0; p < count; ++p) bad += st[p] != 0;
+        for (int p = 0; p < count && !align_failed; ++p) bad += st[p] != 0;
     }
     if (youth_dist_allgather_poses_host(d, T, n, all) != YOUTH_OK) {
         fprintf(stderr, "rank %d: gather: %s\n", rank, youth_dist_last_error());
         return 7;
+    }
+    if (align_failed) {
+        youth_dist_destroy(d);
+        return 6;
     }
     FILE* f = fopen(argv[5], "wb");
     if (!f || fwrite(all, sizeof(float), (size_t)n * 16, f) != (size_t)n * 16) return 8;

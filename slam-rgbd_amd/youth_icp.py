@@ -34,8 +34,8 @@ YOUTH_ENOMEM = -2
 YOUTH_EHIP = -3
 YOUTH_ENODEV = -4
 YOUTH_NEQ = 29
-SPEC_FMA = 0       # YOUTH_SPEC_FMA: spec a7/a8 on fma chains
-SPEC_SURVEY = 1    # YOUTH_SPEC_SURVEY: SURVEY.md §8a a7/a8 as worded (no FMA, IEEE division)
+SPEC_FMA = 0       # YOUTH_SPEC_FMA: opt-in, spec a7/a8 on fma chains
+SPEC_SURVEY = 1    # YOUTH_SPEC_SURVEY (default): SURVEY.md §8a a7/a8 as worded (no FMA, IEEE division)
 STATUS_DEGENERATE = 1
 STATUS_FEW_MATCHES = 2
 

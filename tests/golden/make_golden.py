@@ -9,13 +9,14 @@ Provenance, case by case:
     vectors pinned to the REFERENCE; they are written out here verbatim.
   * pair_* / seq_* — inputs from the synthetic depth source
     (libyouth_synth.so), expected outputs from the C oracle
-    (oracle/liboracle.so) in its default spec (ORACLE_SPEC_FMA).
-  * survey/pair_* / survey/seq_* — the same cases with spec a7/a8 as
-    SURVEY.md §8a words it (ORACLE_SPEC_SURVEY: no FMA, IEEE division).  The
-    committed files are the round-1 fixtures, written by the round-1 oracle
-    before the fma spec existed (git 1041b06^:tests/golden/); `--survey`
-    regenerates them with today's oracle and must leave their arrays equal
-    (tests/test_oracle.py checks it without writing).  The reference has no ICP, so
+    (oracle/liboracle.so) in its default spec, spec a7/a8 as SURVEY.md §8a
+    words it (ORACLE_SPEC_SURVEY: no FMA, IEEE division).  The committed
+    files are the round-1 fixtures, written by the round-1 oracle before the
+    fma spec existed (identical to git 1041b06^:tests/golden/); running this
+    script regenerates them with today's oracle and leaves their arrays
+    equal (tests/test_oracle.py checks that without writing).
+  * fma/pair_* / fma/seq_* — the same cases in the opt-in fma spec
+    (ORACLE_SPEC_FMA, `--fma`).  The reference has no ICP, so
     these pin this build's own spec against regressions: "parity unpinned"
     with respect to the reference beyond back-projection.
 
@@ -119,10 +120,10 @@ SEQ_CASES = [("seq_128x96", 128, 96, 6)]
 
 
 def main():
-    if "--survey" in sys.argv:
-        out = os.path.join(HERE, "survey")
+    if "--fma" in sys.argv:
+        out = os.path.join(HERE, "fma")
         os.makedirs(out, exist_ok=True)
-        with oracle.spec("survey"):
+        with oracle.spec("fma"):
             for args in PAIR_CASES:
                 make_pair_case(*args, out=out)
             for args in SEQ_CASES:
@@ -131,10 +132,11 @@ def main():
     make_recording("rec_24x16_3f.bin")
     np.savez_compressed(os.path.join(HERE, "kat_backproject.npz"),
                         table=np.array(KAT, dtype=np.int64))
-    for args in PAIR_CASES:
-        make_pair_case(*args)
-    for args in SEQ_CASES:
-        make_seq_case(*args)
+    with oracle.spec("survey"):
+        for args in PAIR_CASES:
+            make_pair_case(*args)
+        for args in SEQ_CASES:
+            make_seq_case(*args)
 
 
 if __name__ == "__main__":

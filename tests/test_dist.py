@@ -49,7 +49,10 @@ def _worker(rank, world, port, q):
                   for r in range(world)]
         rows_k = youth_dist.gather_ragged(torch.from_numpy(rel.reshape(-1, 16)), world, 8, counts)
         assert torch.equal(rows, rows_k)
-        q.put((rank, allp.numpy(), (f0, f1), rows.numpy()))
+        # bench.py's N > 1 self-report: the group's size and every rank's times
+        rep = youth_dist.rank_report({"k_icp_ms": 1.0 + rank, "k_prep_ms": 0.1 * rank,
+                                      "gather_ms": 0.01}, world)
+        q.put((rank, allp.numpy(), (f0, f1), rows.numpy(), rep))
     finally:
         dist.destroy_process_group()
 
@@ -65,8 +68,12 @@ def test_world2_gloo_shards_and_gather():
         p.start()
     res = {}
     for _ in range(world):
-        rank, allp, rng, rows = q.get(timeout=240)
+        rank, allp, rng, rows, rep = q.get(timeout=240)
         res[rank] = (allp, rng, rows)
+        assert rep["rccl_world_size"] == world and rep["backend"] == "gloo"
+        assert rep["per_rank_ms"]["k_icp_ms"] == [1.0, 2.0]
+        assert rep["per_rank_ms"]["k_prep_ms"] == [0.0, 0.1]
+        assert rep["per_rank_ms"]["gather_ms"] == [0.01, 0.01]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -81,6 +88,11 @@ def test_world2_gloo_shards_and_gather():
     _, Twc = youth_synth.sequence(0, 9, 64, 48)
     traj = youth_dist.compose_trajectory(rows.reshape(8, 4, 4))
     assert np.allclose(traj, np.linalg.inv(Twc[0]) @ Twc, atol=1e-12)
+
+
+def test_rank_report_without_group():
+    rep = youth_dist.rank_report({"k_icp_ms": 2.5}, 1)
+    assert rep == {"rccl_world_size": 1, "backend": None, "per_rank_ms": {"k_icp_ms": [2.5]}}
 
 
 def test_sequence_shard_edge_cases():

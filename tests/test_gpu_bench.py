@@ -62,10 +62,24 @@ def test_bench_single_gpu_contract():
     assert c2["value"] > 0 and c2["status"] == 0 and c2["pose_max_abs_err_vs_cpu"] <= 1e-5
     assert c2["kernel_path"]["kernel"] == "k_icp_coop"
     assert d["c3"]["parity_ok"] and d["c3"]["batch"]["pairs_per_call"] == 2
+    for tag in ("single_pair", "batch"):
+        rf3 = d["c3"][tag]["roofline"]
+        assert rf3["unit"] == "GB/s" and 0 < rf3["frac"] < 1.0 and rf3["launches"] > 0
     assert d["c5"]["parity_ok"] and d["c5"]["batch"]["trajectory_frames"] == 41
     assert d["c5"]["streamed"]["max_abs_diff_vs_batch_poses"] <= 1e-5
     assert d["kernel_path"]["kernel"].startswith("k_prep + k_icp")
     assert d["viewer_cloud"]["bit_exact_vs_cpu"]
+    # spec a7/a8: the default is SURVEY §8a as worded; both arithmetics
+    # against the survey-spec oracle and their own
+    assert d["spec"]["name"] == "survey"
+    sp = d["spec_parity"]
+    for case in ("c2_64_pairs", "c3_2_pairs_1280x960_20it", "c5_200_pairs",
+                 "survey_noise_16_pairs"):
+        assert sp[case]["gpu_survey_vs_survey_oracle"] <= 1e-5, case
+        assert sp[case]["gpu_fma_vs_fma_oracle"] <= 1e-5, case
+    assert sp["default_within_tol_of_survey_spec"]
+    assert sp["other_spec_rate"]["spec"] == "fma" and sp["other_spec_rate"]["value"] > 0
+    assert d["ranks"]["rccl_world_size"] == 1 and d["ranks"]["per_rank_ms"]["k_icp_ms"][0] > 0
 
 
 @pytest.mark.parametrize("workload", ["pairs", "sequence"])
@@ -87,6 +101,11 @@ def test_bench_two_ranks_rehearsal(workload):
     else:
         assert d["scaling"] == "strong" and d["config"]["pairs"] == 40
     assert "cpu_baseline" not in d          # rank 0 at N=1 only
+    rk = d["ranks"]                         # the N > 1 line's self-report
+    assert rk["rccl_world_size"] == 2 and rk["backend"] == "gloo" and rk["gather_timed"]
+    for k in ("k_icp_ms", "k_prep_ms", "gather_ms"):
+        assert len(rk["per_rank_ms"][k]) == 2, k
+    assert min(rk["per_rank_ms"]["k_icp_ms"]) > 0
 
 
 @pytest.mark.parametrize("workload", ["pairs", "sequence"])
@@ -107,3 +126,5 @@ def test_bench_rccl_gather_one_gpu(workload):
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json_line(r.stdout)
     assert d["n_gpus"] == 1 and d["value"] > 0
+    assert d["ranks"]["rccl_world_size"] == 1 and d["ranks"]["backend"] == "nccl"
+    assert d["ranks"]["gather_timed"] and d["ranks"]["per_rank_ms"]["gather_ms"][0] > 0

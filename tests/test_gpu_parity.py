@@ -846,7 +846,11 @@ def test_headline_512_pairs_one_launch():
     assert float(err.max()) <= POSE_TOL, (int(err.argmax()), float(err.max()))
     assert np.array_equal(Tout, T32)
     assert np.array_equal(cnt, stats[..., 0]), np.argwhere(cnt != stats[..., 0])[:4]
-    np.testing.assert_allclose(r2, stats[..., 1], rtol=1e-9)
+    # sum r^2 of an iteration: fp64 summation order, and the fp32 pose of the
+    # iteration is (float)T64, which can land one ulp apart when T64 differs
+    # in its last bits next to an fp32 rounding boundary (seen once in 5120
+    # pair-iterations: rel 1.3e-9)
+    np.testing.assert_allclose(r2, stats[..., 1], rtol=1e-6)
     K = oracle.viewer_K(W, H)
     with youth_icp.IcpContext(W, H, 2) as ctx:
         for p in (0, 255, 256, 511):

@@ -221,18 +221,18 @@ def test_viewer_cloud_pinned_to_kat():
 
 
 # ------------------------------------------------ SURVEY §8a a7/a8 as worded --
-SURVEY_GOLDEN = os.path.join(GOLDEN, "survey")
+FMA_GOLDEN = os.path.join(GOLDEN, "fma")
 
 
 @pytest.mark.parametrize("name", PAIR_CASES)
 def test_survey_spec_reproduces_round1_fixtures(name):
     """ORACLE_SPEC_SURVEY (no FMA, IEEE division: SURVEY.md §8a a7/a8, §7)
     reproduces, bit for bit, the fixtures the round-1 oracle committed before
-    the fma spec existed (git 1041b06^:tests/golden/, kept verbatim under
-    tests/golden/survey/): association at identity and at the final pose,
-    the identity normal equations, per-iteration stats and the final pose.
-    So the survey spec is a fixed point the kernels did not move."""
-    g = np.load(os.path.join(SURVEY_GOLDEN, name + ".npz"), allow_pickle=False)
+    the fma spec existed (git 1041b06^:tests/golden/, the default fixtures
+    again): association at identity and at the final pose, the identity
+    normal equations, per-iteration stats and the final pose.  So the survey
+    spec is a fixed point the kernels did not move."""
+    g = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
     K, d, it = _K(g["K"]), float(g["dist_thresh"]), int(g["iters"])
     I12 = np.eye(4, dtype=np.float32)[:3]
     with oracle.spec("survey"):
@@ -241,19 +241,27 @@ def test_survey_spec_reproduces_round1_fixtures(name):
         idx0 = oracle.associate(g["src"], g["dst"], I12, K, d)
         neq0 = oracle.reduce(g["src"], g["dst"], I12, K, d)
         idxF = oracle.associate(g["src"], g["dst"], g["T32"], K, d)
-    assert oracle.get_spec() == oracle.SPEC_FMA
+    assert oracle.get_spec() == oracle.SPEC_SURVEY   # the default
     assert st == int(g["status"])
     assert np.array_equal(T64, g["T64"]) and np.array_equal(T32, g["T32"])
     assert np.array_equal(stats, g["stats"])
     assert np.array_equal(idx0, g["idx_identity"]) and np.array_equal(idxF, g["idx_final"])
     assert np.array_equal(neq0.view(np.uint64), g["neq_identity"].view(np.uint64))
-    # the default spec differs from it (else this test would prove nothing)
-    T64f, _, _, _ = oracle.align(g["src"], g["dst"], K, it, d)
+    # the fma spec differs from it (else this test would prove nothing) and
+    # reproduces its own fixtures (tests/golden/fma/)
+    gf = np.load(os.path.join(FMA_GOLDEN, name + ".npz"), allow_pickle=False)
+    with oracle.spec("fma"):
+        T64f, T32f, stf, statsf = oracle.align(g["src"], g["dst"], K, it, d)
+        neqf = oracle.reduce(g["src"], g["dst"], I12, K, d)
+        idxf = oracle.associate(g["src"], g["dst"], gf["T32"], K, d)
     assert not np.array_equal(T64f, g["T64"])
+    assert np.array_equal(T64f, gf["T64"]) and np.array_equal(statsf, gf["stats"])
+    assert np.array_equal(neqf.view(np.uint64), gf["neq_identity"].view(np.uint64))
+    assert np.array_equal(idxf, gf["idx_final"])
 
 
 def test_survey_spec_reproduces_round1_sequence_fixture():
-    g = np.load(os.path.join(SURVEY_GOLDEN, "seq_128x96.npz"), allow_pickle=False)
+    g = np.load(os.path.join(GOLDEN, "seq_128x96.npz"), allow_pickle=False)
     K, d, it = _K(g["K"]), float(g["dist_thresh"]), int(g["iters"])
     f = g["frames"]
     with oracle.spec("survey"):
@@ -265,7 +273,7 @@ def test_survey_spec_reproduces_round1_sequence_fixture():
 def test_set_spec_rejects_unknown():
     with pytest.raises(ValueError):
         oracle.set_spec(7)
-    assert oracle.get_spec() == oracle.SPEC_FMA
+    assert oracle.get_spec() == oracle.SPEC_SURVEY
 
 
 def test_batch_stats_equal_single_align():
@@ -280,17 +288,18 @@ def test_batch_stats_equal_single_align():
 
 
 def test_fma_spec_distance_from_survey_spec():
-    """How far the default (fma) spec's poses sit from SURVEY §8a's literal
-    arithmetic, on 640x480 pairs at the bench's noise
-    and at SURVEY §8d's noise model.  Reported, and bounded loosely: the two
-    specs re-associate pixels on projection / gate boundaries differently,
-    which moves a pose by ~1e-7..1e-5 (DESIGN.md §2 records the full table
-    incl. C3 and C5); the kernels run either spec bit-exact to the oracle."""
+    """How far the opt-in fma spec's poses sit from SURVEY §8a's literal
+    arithmetic (the default), on 640x480 pairs at the
+    bench's noise and at SURVEY §8d's noise model.  Reported, and bounded
+    loosely: the two specs re-associate pixels on projection / gate
+    boundaries differently, which moves a pose by ~1e-7..1e-5 (DESIGN.md §2
+    records the full table incl. C3 and C5); the kernels run either spec
+    bit-exact to the oracle in the same spec."""
     for flags, n in ((youth_synth.DEFAULT_FLAGS, 8), (youth_synth.SURVEY_FLAGS, 8)):
         src, dst, _ = youth_synth.pairs(0, n, flags=flags)
-        Tf, _ = oracle.align_batch(src, dst, iters=10)
-        with oracle.spec("survey"):
-            Ts, _ = oracle.align_batch(src, dst, iters=10)
+        Ts, _ = oracle.align_batch(src, dst, iters=10)
+        with oracle.spec("fma"):
+            Tf, _ = oracle.align_batch(src, dst, iters=10)
         delta = float(np.abs(Tf[:, :3, :4] - Ts[:, :3, :4]).max())
         print(f"flags {flags}: max |T_fma - T_survey| = {delta:.3e}")
         assert 0 < delta < 1e-4
