@@ -267,14 +267,18 @@ int youth_icp_get_plan(youth_icp_ctx* ctx, int* workgroups_per_pair, int* px_per
 int youth_icp_selftest_projdiv(int device, long long n, unsigned long long seed,
                                long long* bit_mismatches, long long* proj_mismatches);
 
-/* Validation of YOUTH_SPEC_SURVEY's projection quotient (the correctly
- * rounded reciprocal plus ONE correction step) against IEEE num / den on n
- * seeded cases: *quot_mismatches bitwise with den in [2^-60, 2^60], half of
- * them next to a rounding midpoint; *proj_mismatches of the projected pixel
- * floor((q + c) + 0.5) or its in-range test, den over the whole positive
- * range.  Both must be 0. */
+/* Validation of YOUTH_SPEC_SURVEY's projection (the correctly rounded
+ * reciprocal plus ONE correction step for the quotient, one
+ * v_cvt_flr_i32_f32 for the floor) against IEEE num / den and floorf:
+ * *quot_mismatches bitwise on n seeded cases with den in [2^-60, 2^60], half
+ * of them next to a rounding midpoint; *proj_mismatches of the projected
+ * pixel floor((q + c) + 0.5) or its in-range test on n cases, den over the
+ * whole positive range; *floor_mismatches of the one-instruction floor over
+ * all 2^32 bit patterns (NaN and denormals excluded: the projection never
+ * forms them).  All must be 0. */
 int youth_icp_selftest_projquot(int device, long long n, unsigned long long seed,
-                                long long* quot_mismatches, long long* proj_mismatches);
+                                long long* quot_mismatches, long long* proj_mismatches,
+                                long long* floor_mismatches);
 
 /* Self-test of the target-normal normalisation's fast path (correctly rounded
  * sqrt without rescaling, three quotients sharing one reciprocal) against

@@ -194,6 +194,22 @@ __device__ __forceinline__ float proj_quot(float n, float den, float r)
     return fmaf(fmaf(-den, q0, n), r, q0);
 }
 
+// (int)floorf(x) in one instruction (v_cvt_flr_i32_f32; floorf + the int
+// conversion are two 4-cycle VALU forms, profiles/r03/valu_cycles.txt).
+// Equal to (int)floorf(x) for every normal or zero x with |x| < 2^30, and
+// (unsigned) of it < 16384 exactly when 0 <= floorf(x) < 16384 for every
+// non-NaN x but denormals (saturating conversion): youth_icp_selftest_projquot
+// checks both over all 2^32 bit patterns.  kSpecSurvey's projected
+// coordinate ((q + c) + 0.5) is never NaN (T finite, q finite or +-inf) and
+// never denormal (it is 0 or at least 2^-25 in magnitude: s + 0.5 with s a
+// float near -0.5 is exact by Sterbenz, |s| < 0.25 leaves it above 0.25).
+__device__ __forceinline__ int floor_i32(float x)
+{
+    int r;
+    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
 // Spec a6's normalisation n = c / sqrtf(|c|^2) on its common range, bit for
 // bit.  hipcc's correctly rounded sqrtf is  x' = x < 2^-96 ? x 2^32 : x;
 // s = v_sqrt(x'); s -= (fma(-(s-1ulp), s, x') <= 0); s += (fma(-(s+1ulp), s,
@@ -333,7 +349,11 @@ __global__ void k_selftest_projdiv(unsigned long long n, unsigned long long seed
 //   bad[1]: mismatches of the projected pixel floor((q + c) + 0.5) and its
 //           in-range test [0, 65536), den anywhere in the positive finite
 //           fp32 range (outside the guard the kernels divide with IEEE),
-//           c in [0, 4096): must be 0 for both.
+//           c in [0, 4096): must be 0 for both;
+//   bad[2]: floor_i32 against (int)floorf over ALL 2^32 bit patterns except
+//           NaN and denormals: value mismatches where |x| < 2^30, and
+//           in-range disagreements ((unsigned)r < 16384 vs 0 <= floorf(x) <
+//           16384) anywhere: must be 0.
 __device__ __forceinline__ float survey_quot(float n, float den)
 {
     if (proj_den_ok(den)) return proj_quot(n, den, proj_recip(den));
@@ -387,8 +407,19 @@ __global__ void k_selftest_projquot(unsigned long long n, unsigned long long see
             if (ii != inf_ || (ii && ui != uf)) ++b1;
         }
     }
+    unsigned long long b2 = 0;
+    for (unsigned long long b = tid; b < (1ull << 32); b += stride) {
+        const float x = __uint_as_float((unsigned)b);
+        if (x != x || (x != 0.0f && fabsf(x) < 0x1p-126f)) continue;  // NaN, denormal
+        const float f = floorf(x);
+        const int r = floor_i32(x);
+        const bool in_ref = (f >= 0.0f) & (f < 16384.0f);
+        const bool in_got = (unsigned)r < 16384u;
+        b2 += (in_ref != in_got) || (fabsf(x) < 0x1p30f && r != (int)f);
+    }
     if (b0) atomicAdd(bad + 0, b0);
     if (b1) atomicAdd(bad + 1, b1);
+    if (b2) atomicAdd(bad + 2, b2);
 }
 
 // Self-test of k_prep's fast normalisation (sqrt_rn_mid, norm_div):
@@ -619,11 +650,23 @@ __device__ __forceinline__ void init_pairs(const InitArgs& ia, int tx, int ty, i
 // tile's horizontal and vertical halo lines belong to tiles that the same
 // XCD processes at about the same time, i.e. are hits in that XCD's L2
 // instead of fetches of lines that neighbouring tiles on other XCDs own.
+// xcd_map = 2: each XCD takes whole rows of tiles, rows dealt round-robin
+// (row R on XCD R % 8, its tiles in order), so the 8 XCDs work on 8
+// adjacent tile rows of one frame at a time: a tile's horizontal halo lines
+// belong to its own row (same XCD) and only the top / bottom halo rows (2 of
+// 50) come from another XCD's row.  The grid is padded to a multiple of 8
+// rows x tiles_x; padding workgroups return -1.
 // xcd_map = 0: t = b (row-major over the frames: neighbours on other XCDs).
 __device__ __forceinline__ int xcd_tile(int b, int total)
 {
     const int q = total >> 3, r = total & 7, x = b & 7, j = b >> 3;
     return x < r ? x * (q + 1) + j : r * (q + 1) + (x - r) * q + j;
+}
+__device__ __forceinline__ int xcd_row_tile(int b, int tiles_x, int rows)
+{
+    const int j = b >> 3;
+    const int R = (j / tiles_x) * 8 + (b & 7);
+    return R < rows ? R * tiles_x + (j - (j / tiles_x) * tiles_x) : -1;
 }
 
 template <bool kFast, bool kWide>
@@ -635,7 +678,10 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const int16_t* __restrict
                                                       int xcd_map)
 {
     const int total = tiles_x * tiles_y * n_frames;
-    const int t = xcd_map ? xcd_tile((int)blockIdx.x, total) : (int)blockIdx.x;
+    const int t = xcd_map == 1   ? xcd_tile((int)blockIdx.x, total)
+                  : xcd_map == 2 ? xcd_row_tile((int)blockIdx.x, tiles_x, tiles_y * n_frames)
+                                 : (int)blockIdx.x;
+    if (t < 0) return;  // grid padding (xcd_map 2)
     const int per = tiles_x * tiles_y;
     const int f = t / per;
     const int r = t - f * per;
@@ -1065,8 +1111,17 @@ __device__ __forceinline__ void xform_project(const float* T, float sx, float sy
             pu = nu / den;
             pv = nv / den;
         }
-        uu = floorf((pu + K.cx) + 0.5f);
-        vv = floorf((pv + K.cy) + 0.5f);
+        // floor, in-range test and the pixel index without selects: the
+        // coordinates stay finite on every lane (saturated integers), and an
+        // unmatched lane's gather is masked after it (a raw buffer load past
+        // the records returns 0, any index inside them is a real record)
+        const int iu = floor_i32((pu + K.cx) + 0.5f);
+        const int iv = floor_i32((pv + K.cy) + 0.5f);
+        in = vz & ((unsigned)iu < (unsigned)W) & ((unsigned)iv < (unsigned)H);
+        fu = (float)iu;
+        fv = (float)iv;
+        j = (int)(__umul24((unsigned)iv, (unsigned)W) + (unsigned)iu);
+        return;
     } else {
         qx = fmaf(T[2], sz, fmaf(T[1], sy, fmaf(T[0], sx, T[3])));
         qy = fmaf(T[6], sz, fmaf(T[5], sy, fmaf(T[4], sx, T[7])));
@@ -1201,7 +1256,7 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
         f4v t[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-            t[q] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rrec, j[q] * 16,
+            t[q] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rrec, (int)((unsigned)j[q] * 16u),
                                                                                  0, 0));
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -1791,7 +1846,7 @@ __device__ __forceinline__ void coop_group(const float* __restrict__ X, const fl
     f4v rec[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q)
-        rec[q] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rrec, j[q] * 16, 0, 0));
+        rec[q] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rrec, (int)((unsigned)j[q] * 16u), 0, 0));
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
         const bool ok = match_accumulate<kSp, kFast>(qx[q], qy[q], qz[q], rec[q], fu[q], fv[q],
@@ -2309,7 +2364,8 @@ static int launch_prep(youth_icp_ctx* c, hipStream_t s, const int16_t* depth, in
         if (rc) return rc;
     }
     const int tiles_x = (c->W + kTileW - 1) / kTileW, tiles_y = (c->H + kTileH - 1) / kTileH;
-    const long long blocks = (long long)tiles_x * tiles_y * n_frames;
+    const long long rows = (long long)tiles_y * n_frames;
+    const long long blocks = (long long)tiles_x * (c->prep_xcd_map == 2 ? (rows + 7) / 8 * 8 : rows);
     if (blocks > 0x7fffffffLL) return set_error(YOUTH_EINVAL, "launch_prep: %lld tiles", blocks);
     EventPair ep{};
     int rc = ev_begin(c, s, &ep, 2);
@@ -2926,7 +2982,7 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         const char* crf = getenv("YOUTH_ICP_TEST_REFUSE_COOP");
         c->coop_refuse = crf && *crf && *crf != '0';
         const char* pxm = getenv("YOUTH_ICP_PREP_XCD_MAP");
-        if (pxm && *pxm == '1') c->prep_xcd_map = 1;
+        if (pxm && (*pxm == '1' || *pxm == '2')) c->prep_xcd_map = *pxm - '0';
         const char* cts = getenv("YOUTH_ICP_COOP_TILE_SRC");
         if (cts && *cts == '0') c->coop_tile_src = false;
         const char* cmp = getenv("YOUTH_ICP_COOP_MAX_PAIRS");
@@ -3088,7 +3144,8 @@ int youth_icp_selftest_projdiv(int device, long long n, unsigned long long seed,
 }
 
 int youth_icp_selftest_projquot(int device, long long n, unsigned long long seed,
-                                long long* quot_mismatches, long long* proj_mismatches)
+                                long long* quot_mismatches, long long* proj_mismatches,
+                                long long* floor_mismatches)
 {
     if (n < 0) return set_error(YOUTH_EINVAL, "selftest_projquot: n < 0");
     const int ndev = youth_icp_device_count();
@@ -3096,8 +3153,8 @@ int youth_icp_selftest_projquot(int device, long long n, unsigned long long seed
         return set_error(YOUTH_ENODEV, "selftest_projquot: no HIP device %d", device);
     HIP_TRY(hipSetDevice(device));
     unsigned long long* d_bad = nullptr;
-    HIP_TRY(hipMalloc(&d_bad, 2 * sizeof(unsigned long long)));
-    unsigned long long h[2] = {0, 0};
+    HIP_TRY(hipMalloc(&d_bad, 3 * sizeof(unsigned long long)));
+    unsigned long long h[3] = {0, 0, 0};
     hipError_t e = hipMemset(d_bad, 0, sizeof(h));
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_selftest_projquot, dim3(4096), dim3(256), 0, 0,
@@ -3109,6 +3166,7 @@ int youth_icp_selftest_projquot(int device, long long n, unsigned long long seed
     if (e != hipSuccess) return set_error(YOUTH_EHIP, "selftest_projquot: %s", hipGetErrorString(e));
     if (quot_mismatches) *quot_mismatches = (long long)h[0];
     if (proj_mismatches) *proj_mismatches = (long long)h[1];
+    if (floor_mismatches) *floor_mismatches = (long long)h[2];
     return YOUTH_OK;
 }
 

@@ -89,6 +89,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "youth_icp_get_spec": (c_int, [c_void_p]),
         "youth_icp_selftest_projquot": (c_int, [c_int, ctypes.c_longlong, ctypes.c_ulonglong,
                                                 POINTER(ctypes.c_longlong),
+                                                POINTER(ctypes.c_longlong),
                                                 POINTER(ctypes.c_longlong)]),
         "youth_icp_align_batch": (c_int, [P16, P16, c_int, c_int, c_int, POINTER(Intrinsics),
                                           c_int, PF, PI32]),
@@ -502,13 +503,15 @@ def selftest_projdiv(n: int, seed: int = 1, device: int = 0) -> tuple[int, int]:
     return b.value, p.value
 
 
-def selftest_projquot(n: int, seed: int = 1, device: int = 0) -> tuple[int, int]:
-    """youth_icp_selftest_projquot: (quotient mismatches, projection mismatches)
-    of YOUTH_SPEC_SURVEY's projection quotient vs IEEE num / den on n cases."""
+def selftest_projquot(n: int, seed: int = 1, device: int = 0) -> tuple[int, int, int]:
+    """youth_icp_selftest_projquot: (quotient mismatches, projection mismatches,
+    one-instruction floor mismatches over all 2^32 floats) of
+    YOUTH_SPEC_SURVEY's projection vs IEEE num / den and floorf."""
     lib = load_library()
-    q, p = ctypes.c_longlong(0), ctypes.c_longlong(0)
-    _check(lib.youth_icp_selftest_projquot(device, n, seed, ctypes.byref(q), ctypes.byref(p)))
-    return q.value, p.value
+    q, p, f = ctypes.c_longlong(0), ctypes.c_longlong(0), ctypes.c_longlong(0)
+    _check(lib.youth_icp_selftest_projquot(device, n, seed, ctypes.byref(q), ctypes.byref(p),
+                                           ctypes.byref(f)))
+    return q.value, p.value, f.value
 
 
 def selftest_normalize(n: int, seed: int = 1, device: int = 0) -> tuple[int, int, int]:

@@ -856,3 +856,30 @@ def test_headline_512_pairs_one_launch():
         for p in (0, 255, 256, 511):
             g_idx, _ = ctx.reduce(src[p], dst[p], T32[p][:3])
             assert np.array_equal(g_idx, oracle.associate(src[p], dst[p], T32[p][:3], K)), p
+
+
+@pytest.mark.parametrize("xcd_map", ["1", "2"])
+def test_prep_tile_orders_bit_identical(xcd_map, monkeypatch):
+    """k_prep's workgroup -> tile orders (YOUTH_ICP_PREP_XCD_MAP: 0 row-major
+    over the frames, 1 one contiguous run per XCD, 2 tile rows dealt over the
+    XCDs with a padded grid) only reorder the tiles: records and the aligned
+    poses equal the default order's bit for bit, frames whose tile-row count
+    is not a multiple of 8 included (97x53: 2 x 2 tiles)."""
+    import torch
+    for W, H, n in ((640, 480, 12), (97, 53, 5)):
+        src, dst, _ = youth_synth.pairs(40, n, W, H)
+        ds, dd = torch.from_numpy(src).cuda(), torch.from_numpy(dst).cuda()
+        torch.cuda.synchronize()
+        out = {}
+        for m in ("0", xcd_map):
+            monkeypatch.setenv("YOUTH_ICP_PREP_XCD_MAP", m)
+            monkeypatch.setenv("YOUTH_ICP_NO_COOP", "1")
+            with youth_icp.IcpContext(W, H, n) as ctx:
+                rec = ctx.prepare(dst, want_normals=True, want_xyz=False)
+                ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), n)
+                T64, _, st = ctx.get_poses(n)
+            out[m] = (rec, T64, st)
+        for a, b in zip(out["0"][0][3:], out[xcd_map][0][3:]):
+            assert np.array_equal(_bits(a), _bits(b))
+        assert np.array_equal(out["0"][1], out[xcd_map][1])
+        assert np.array_equal(out["0"][2], out[xcd_map][2]) and not out["0"][2].any()

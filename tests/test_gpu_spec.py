@@ -39,9 +39,11 @@ def _err(a, b):
 def test_projquot_selftest():
     """The survey projection's quotient (correctly rounded reciprocal + one
     correction) equals IEEE num / den bitwise on 2^27 cases (half next to a
-    rounding midpoint) and projects to the same pixel on 2^27 more."""
-    q, p = youth_icp.selftest_projquot(1 << 27, seed=3)
-    assert (q, p) == (0, 0)
+    rounding midpoint) and projects to the same pixel on 2^27 more; its
+    one-instruction floor equals floorf (and its in-range test) on all 2^32
+    floats but NaN and denormals."""
+    q, p, f = youth_icp.selftest_projquot(1 << 27, seed=3)
+    assert (q, p, f) == (0, 0, 0)
 
 
 def test_spec_selection_api(monkeypatch):

@@ -9,12 +9,14 @@ NAME=$1; SRC=$2
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$ROOT/tools/ab/$NAME
 mkdir -p $OUT
-if [ -f "$SRC" ]; then cp "$SRC" $OUT/icp_kernels.hip
-else git -C $ROOT show "$SRC:slam-rgbd_amd/csrc/icp_kernels.hip" > $OUT/icp_kernels.hip; fi
+mkdir -p $OUT/include
+if [ -f "$SRC" ]; then cp "$SRC" $OUT/icp_kernels.hip; cp $ROOT/include/youth_icp.h $OUT/include/
+else git -C $ROOT show "$SRC:slam-rgbd_amd/csrc/icp_kernels.hip" > $OUT/icp_kernels.hip
+     git -C $ROOT show "$SRC:include/youth_icp.h" > $OUT/include/youth_icp.h; fi
 cd $ROOT/slam-rgbd_amd
 make -s build/slam_api.o build/algorithm_module.o build/wire.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize \
-    ${HIPFLAGS_EXTRA:-} -I../include -Icsrc -c $OUT/icp_kernels.hip -o $OUT/icp_kernels.o
+    ${HIPFLAGS_EXTRA:-} -I$OUT/include -I../include -Icsrc -c $OUT/icp_kernels.hip -o $OUT/icp_kernels.o
 # the viewer kernels: the tree's, or env VIEWER_SRC (a viewer_cloud.hip variant)
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize \
     -I../include -Icsrc -c ${VIEWER_SRC:-csrc/viewer_cloud.hip} -o $OUT/viewer_cloud.o

@@ -2,8 +2,11 @@
 // (gfx950).  Each wave runs 8 independent dependency chains of ONE
 // instruction form (inline asm, so the compiler cannot re-pack, re-encode or
 // drop it); the chip is filled with 4 waves/SIMD; the printed cost is wall
-// time per wave-instruction per SIMD (ns; x clock = cycles).  The results
-// are the cost model of DESIGN.md §5 (profiles/r01/valu_rate.txt).
+// time per wave-instruction per SIMD (ns) and, with the shader clock of that
+// run (thread 0 of every workgroup reads s_memtime = shader cycles and
+// s_memrealtime = 100 MHz around its loop), cycles per wave-instruction per
+// SIMD.  The results are the cost model of DESIGN.md §5
+// (profiles/r01/valu_rate.txt: ns; profiles/r03/valu_cycles.txt: cycles).
 //
 // Build: hipcc --offload-arch=gfx950 -O3 tools/valu_rate.hip -o tools/valu_rate
 #include <hip/hip_runtime.h>
@@ -20,7 +23,7 @@
         }                                                                             \
     } while (0)
 
-constexpr int kIters = 1024;
+constexpr int kIters = 8192;
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 #define REP8(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
@@ -56,14 +59,23 @@ typedef float f2 __attribute__((ext_vector_type(2)));
         x0 + x7 + y0 + y7 + q0.x + q7.y + r0.x + r7.y + (float)(e0 + e7 + g0 + g7);
 
 // one kernel per form: BODY(k) is the asm statement on chain k
-#define FORM(NAME, BODY)                                                       \
-    __global__ __launch_bounds__(256) void k_##NAME(float* out, float seed)   \
-    {                                                                          \
-        DECL                                                                   \
-        for (int it = 0; it < kIters; ++it) {                                  \
-            _Pragma("unroll") for (int u = 0; u < 8; ++u) { REP8(BODY) }       \
-        }                                                                      \
-        SINK                                                                   \
+#define FORM(NAME, BODY)                                                                  \
+    __global__ __launch_bounds__(256) void k_##NAME(float* out, float seed,              \
+                                                    unsigned long long* clk)             \
+    {                                                                                     \
+        DECL                                                                              \
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();                       \
+        const unsigned long long rt0_ = __builtin_amdgcn_s_memrealtime();                   \
+        for (int it = 0; it < kIters; ++it) {                                             \
+            _Pragma("unroll") for (int u = 0; u < 8; ++u) { REP8(BODY) }                  \
+        }                                                                                 \
+        const unsigned long long t1 = __builtin_amdgcn_s_memtime();                       \
+        const unsigned long long rt1_ = __builtin_amdgcn_s_memrealtime();                   \
+        if (threadIdx.x == 0) {                                                           \
+            clk[2 * blockIdx.x] = t1 - t0;                                                \
+            clk[2 * blockIdx.x + 1] = rt1_ - rt0_;                                            \
+        }                                                                                 \
+        SINK                                                                              \
     }
 
 #define B_fma(k) asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(a##k) : "v"(c));
@@ -103,6 +115,14 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 #define B_pkfma3(k) asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(p##k) : "v"(q##k), "v"(r##k));
 #define B_pkmul2(k) asm volatile("v_pk_mul_f32 %0, %1, %2" : "=v"(p##k) : "v"(q##k), "v"(r##k));
 #define B_fmac64d(k) asm volatile("v_fmac_f64_e32 %0, %1, %2" : "+v"(d##k) : "v"(e##k), "v"(g##k));
+#define B_fmac3(k) asm volatile("v_fmac_f32_e32 %0, %1, %2" : "+v"(a##k) : "v"(x##k), "v"(y##k));
+#define B_mul2(k) asm volatile("v_mul_f32_e32 %0, %1, %2" : "=v"(a##k) : "v"(x##k), "v"(y##k));
+#define B_cnd64d(k) asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(a##k) : "v"(x##k), "v"(y##k), "s"(m));
+#define B_floor2(k) asm volatile("v_floor_f32_e32 %0, %1" : "=v"(a##k) : "v"(x##k));
+#define B_cvtif2(k) asm volatile("v_cvt_i32_f32_e32 %0, %1" : "=v"(a##k) : "v"(x##k));
+#define B_cvt64d(k) asm volatile("v_cvt_f64_f32_e32 %0, %1" : "=v"(d##k) : "v"(x##k));
+#define B_mu24(k) asm volatile("v_mul_u32_u24_e32 %0, %1, %2" : "=v"(a##k) : "v"(x##k), "v"(y##k));
+#define B_and(k) asm volatile("v_and_b32_e32 %0, %1, %2" : "=v"(a##k) : "v"(x##k), "v"(y##k));
 #define B_cmpcnd(k)                                                                       \
     asm volatile("v_cmp_lt_f32_e32 vcc, %1, %2\n\tv_cndmask_b32_e32 %0, %0, %2, vcc"     \
                  : "+v"(a##k) : "v"(x##k), "v"(y##k) : "vcc");
@@ -145,6 +165,14 @@ FORM(pkmul2, B_pkmul2)
 FORM(fmac64d, B_fmac64d)
 FORM(cmpcnd, B_cmpcnd)
 FORM(cmpcnd64, B_cmpcnd64)
+FORM(fmac3, B_fmac3)
+FORM(mul2, B_mul2)
+FORM(cnd64d, B_cnd64d)
+FORM(floor2, B_floor2)
+FORM(cvtif2, B_cvtif2)
+FORM(cvt64d, B_cvt64d)
+FORM(mu24, B_mu24)
+FORM(andb, B_and)
 
 int main()
 {
@@ -153,9 +181,12 @@ int main()
     const int blocks = cus * 4;  // 4 workgroups x 4 waves per CU -> 4 waves/SIMD
     float* out;
     CK(hipMalloc(&out, (size_t)blocks * 256 * 4));
+    unsigned long long* clk;
+    CK(hipMalloc(&clk, (size_t)blocks * 2 * sizeof(unsigned long long)));
+    unsigned long long* hclk = (unsigned long long*)malloc((size_t)blocks * 2 * sizeof(unsigned long long));
     struct F {
         const char* name;
-        void (*k)(float*, float);
+        void (*k)(float*, float, unsigned long long*);
     } forms[] = {{"v_fma_f32 (VOP3)", k_fma},
                  {"v_fmac_f32_e32 (VOP2)", k_fmac},
                  {"v_mul_f32_e32", k_mul},
@@ -187,22 +218,41 @@ int main()
                  {"v_pk_mul_f32 2 distinct", k_pkmul2},
                  {"v_fmac_f64 distinct", k_fmac64d},
                  {"cmp_e32+cndmask_e32 (x2)", k_cmpcnd},
-                 {"cmp_e64+cndmask_e64 (x2)", k_cmpcnd64}};
+                 {"cmp_e64+cndmask_e64 (x2)", k_cmpcnd64},
+                 {"v_fmac_f32 distinct", k_fmac3},
+                 {"v_mul_f32 distinct", k_mul2},
+                 {"v_cndmask_e64 distinct", k_cnd64d},
+                 {"v_floor_f32 distinct", k_floor2},
+                 {"v_cvt_i32_f32 distinct", k_cvtif2},
+                 {"v_cvt_f64_f32 distinct", k_cvt64d},
+                 {"v_mul_u32_u24 distinct", k_mu24},
+                 {"v_and_b32 distinct", k_andb}};
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     const double inst_per_simd = 4.0 * kIters * 64;
-    printf("%-26s %10s %14s\n", "form", "us", "ns/inst/SIMD");
+    printf("%-26s %10s %14s %8s %16s\n", "form", "us", "ns/inst/SIMD", "GHz", "cycles/inst/SIMD");
     for (auto& f : forms) {
-        hipLaunchKernelGGL(f.k, dim3(blocks), dim3(256), 0, 0, out, 1.0f);
+        hipLaunchKernelGGL(f.k, dim3(blocks), dim3(256), 0, 0, out, 1.0f, clk);
         CK(hipEventRecord(e0));
-        for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(f.k, dim3(blocks), dim3(256), 0, 0, out, 1.0f);
+        for (int r = 0; r < 5; ++r)
+            hipLaunchKernelGGL(f.k, dim3(blocks), dim3(256), 0, 0, out, 1.0f, clk);
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
         float ms;
         CK(hipEventElapsedTime(&ms, e0, e1));
         const double us = ms * 1e3 / 5;
-        printf("%-26s %10.1f %14.3f\n", f.name, us, us * 1e3 / inst_per_simd);
+        // the last run's loop: shader cycles and 100 MHz ticks of every
+        // workgroup's wave 0 (its 4 waves per SIMD run side by side)
+        CK(hipMemcpy(hclk, clk, (size_t)blocks * 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        double cyc = 0, rt = 0;
+        for (int b = 0; b < blocks; ++b) {
+            cyc += (double)hclk[2 * b];
+            rt += (double)hclk[2 * b + 1];
+        }
+        const double ghz = rt > 0 ? cyc / (rt * 10.0) : 0.0;  // realtime ticks are 10 ns
+        printf("%-26s %10.1f %14.3f %8.3f %16.3f\n", f.name, us, us * 1e3 / inst_per_simd, ghz,
+               cyc / blocks / inst_per_simd);
     }
     return 0;
 }
