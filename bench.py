@@ -253,7 +253,14 @@ def roofline_icp(a, kt, n_pairs, W, H):
         out["valu_issue_frac"] = tj["valu_busy_frac"]
         out["valu"] = {k: tj[k] for k in ("valu_busy_frac", "valu_lane_ops_per_px_iteration",
                                           "valu_cycles_per_instruction", "effective_clock_ghz",
-                                          "valu_busy_definition") if k in tj}
+                                          "valu_busy_definition", "wave_state_frac",
+                                          "rocprof_valubusy") if k in tj}
+        if "valu_account" in tj:
+            acc = tj["valu_account"]
+            out["valu"]["busy_frac_range"] = [acc["busy_frac_other_at_2_4_cycles"],
+                                              acc["busy_frac"]]
+            out["valu"]["issue_cycles_by_class_frac"] = {
+                k: v / acc["simd_cycles_available"] for k, v in acc["issue_cycles_by_class"].items()}
     return out
 
 

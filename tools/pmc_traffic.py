@@ -73,9 +73,11 @@ def main():
             # rocprof's derived VALUBusy: 4 x SQ_ACTIVE_INST_VALU (quad-cycles) /
             # SIMDs / GRBM_GUI_ACTIVE (per XCD); ~1 = a VALU instruction in
             # execution on every SIMD in every cycle of the kernel
-            doc["valu_busy_frac"] = 4.0 * r["SQ_ACTIVE_INST_VALU"] / simds / cyc
-            doc["valu_busy_definition"] = ("4 x SQ_ACTIVE_INST_VALU / SIMDs / (GRBM_GUI_ACTIVE / "
-                                           "8 XCDs) (rocprof VALUBusy)")
+            # rocprof's derived VALUBusy (4 x SQ_ACTIVE_INST_VALU / SIMDs /
+            # cycles): SQ_ACTIVE_INST_VALU counts, per wave, the quad-cycles
+            # its VALU instruction is in execution, and the 4 waves of a SIMD
+            # overlap there, so it can exceed 1; not an issue fraction
+            doc["rocprof_valubusy"] = 4.0 * r["SQ_ACTIVE_INST_VALU"] / simds / cyc
         durs = []
         for f in glob.glob(os.path.join(root, "**", "*kernel_trace.csv"), recursive=True):
             if "pmc_sq" not in f:
@@ -86,6 +88,45 @@ def main():
         if durs:
             avg_ns = sum(durs) / len(durs)
             doc["effective_clock_ghz"] = cyc / avg_ns
+    # VALU issue account: instruction classes from the
+    # SQ_INSTS_VALU_* counters x their measured issue cost in SIMD-cycles
+    # (tools/valu_costs.py over tools/valu_rate, the same GRBM normalisation),
+    # against the SIMD-cycles of the launch.  "other" = SQ_INSTS_VALU minus
+    # the classified ones (v_cmp, v_cndmask, v_mov, permlane / readlane / DPP);
+    # its cost is bracketed by the 4.3-cycle compare/select forms and the
+    # 2.4-cycle moves.
+    costs_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                              "profiles", "r03", "valu_costs.json")
+    cls = ["ADD_F32", "MUL_F32", "FMA_F32", "TRANS_F32", "FMA_F64", "ADD_F64", "MUL_F64", "CVT",
+           "INT32", "INT64"]
+    if os.path.exists(costs_path) and all(f"SQ_INSTS_VALU_{c}" in r for c in cls) and \
+            "GRBM_GUI_ACTIVE" in r and "SQ_INSTS_VALU" in r:
+        cost = json.load(open(costs_path))["simd_cycles_per_wave_instruction"]
+        simds = doc.get("simds", 1024)
+        avail = simds * r["GRBM_GUI_ACTIVE"] / N_XCD
+        counts = {c: r[f"SQ_INSTS_VALU_{c}"] for c in cls}
+        counts["other"] = max(0.0, r["SQ_INSTS_VALU"] - sum(counts.values()))
+        cyc = {c: counts[c] * cost[c]["cycles"] for c in counts}
+        lo = sum(cyc.values()) - cyc["other"] + counts["other"] * cost["other_2cycle"]["cycles"]
+        doc["valu_account"] = {
+            "simd_cycles_available": avail,
+            "instructions_by_class": counts,
+            "issue_cycles_by_class": cyc,
+            "issue_cycles": sum(cyc.values()),
+            "busy_frac": sum(cyc.values()) / avail,
+            "busy_frac_other_at_2_4_cycles": lo / avail,
+            "cost_source": os.path.relpath(costs_path, os.path.dirname(os.path.dirname(
+                os.path.abspath(__file__)))),
+        }
+        doc["valu_busy_frac"] = sum(cyc.values()) / avail
+        doc["valu_busy_definition"] = ("sum over VALU classes of SQ_INSTS_VALU_<class> x its "
+                                       "measured issue cost (SIMD-cycles, tools/valu_rate) / "
+                                       "(SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)")
+    if all(k in r for k in ("SQ_WAVE_CYCLES", "SQ_WAIT_INST_ANY")) and "SQ_ACTIVE_INST_ANY" in r:
+        w = r["SQ_WAVE_CYCLES"]
+        doc["wave_state_frac"] = {"active": r["SQ_ACTIVE_INST_ANY"] / w,
+                                  "issue_stalled": r["SQ_WAIT_INST_ANY"] / w,
+                                  "parked": r.get("SQ_WAIT_ANY", float("nan")) / w}
     for k in ("k_prep", "k_solve"):
         m = next((x for x in res if x.startswith(k)), None)
         if m and "FETCH_SIZE" in res[m]:
