@@ -68,6 +68,12 @@ def parse():
     ap.add_argument("--pairs-per-gpu", type=int, default=0,
                     help="> 0: weak scaling with this many pairs per GPU")
     ap.add_argument("--frames", type=int, default=1000, help="sequence workload length")
+    ap.add_argument("--pipeline", type=int, default=0, choices=[0, 1, 2],
+                    help="pairs workload: steps in flight per rank; 2 = two contexts on two "
+                         "streams, so step s+1's k_prep / k_icp fill step s's k_icp tail "
+                         "(independent batches, each completed inside the timed region); "
+                         "0 = auto: 2 for shards of <= 96 pairs (N = 8's 64: +2 %), else 1 "
+                         "(512 / 128 pairs: -1 %; profiles/r03/ab_pipeline.txt)")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
@@ -200,6 +206,22 @@ class Run:
             dist.destroy_process_group()
 
 
+class CtxGroup:
+    """The rank's contexts (one per step in flight) as one for timing:
+    events on every context, times and launch counts summed."""
+
+    def __init__(self, ctxs):
+        self.ctxs = ctxs
+
+    def set_timing(self, enable, iteration_kernel_only=False):
+        for c in self.ctxs:
+            c.set_timing(enable, iteration_kernel_only)
+
+    def get_timing(self, kind=0):
+        t = [c.get_timing(kind) for c in self.ctxs]
+        return sum(x[0] for x in t), sum(x[1] for x in t)
+
+
 def load_pmc(a, W, H):
     """The committed PMC pass of k_icp (tools/profile.sh + tools/pmc_traffic.py):
     HBM bytes and VALU figures per pixel-iteration, valid only for the kernel
@@ -313,28 +335,41 @@ def run_pairs(R):
     host = [torch.zeros((n_glob, 16), dtype=torch.float32).pin_memory()
             for _ in range(2)]
     done = [None, None]
-    ctx = youth_icp.IcpContext(W, H, max(n, 2), iters=a.iters, device=R.local)
+    depth = a.pipeline or (2 if n <= 96 else 1)
+    # --pipeline 2: step s runs on context / stream s % 2 (each context its
+    # own records, poses and queue words), so consecutive steps are
+    # independent and the GPU starts step s+1's kernels as step s's
+    # persistent k_icp retires its workgroups
+    ctxs = [youth_icp.IcpContext(W, H, max(n, 2), iters=a.iters, device=R.local)
+            for _ in range(depth)]
+    ctx = ctxs[0]
+    streams = [main] + [torch.cuda.Stream() for _ in range(depth - 1)]
     it = [0]
 
     def step():
         b = it[0] & 1
+        q = it[0] % depth
         it[0] += 1
-        if done[b] is not None:
-            main.wait_event(done[b])
-        ctx.align_pairs_device(d_src.data_ptr(), d_dst.data_ptr(), n,
-                               d_T_out=poses[b].data_ptr(), stream=main.cuda_stream)
-        work = youth_dist.gather_poses_ragged_async(poses[b], gathered[b], world, counts)
-        with torch.cuda.stream(side):
-            if work is not None:
-                work.wait()                 # side waits for the gather (no host block)
-            else:
-                side.wait_stream(main)
-            host[b].copy_(gathered[b], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(side)
-            done[b] = ev
+        st = streams[q]
+        with torch.cuda.stream(st):
+            if done[b] is not None:
+                st.wait_event(done[b])
+            ctxs[q].align_pairs_device(d_src.data_ptr(), d_dst.data_ptr(), n,
+                                       d_T_out=poses[b].data_ptr(), stream=st.cuda_stream)
+            work = youth_dist.gather_poses_ragged_async(poses[b], gathered[b], world, counts)
+            with torch.cuda.stream(side):
+                if work is not None:
+                    work.wait()             # side waits for the gather (no host block)
+                else:
+                    side.wait_stream(st)
+                host[b].copy_(gathered[b], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(side)
+                done[b] = ev
 
-    elapsed, kt, spread = R.timed(ctx, step)
+    elapsed, kt, spread = R.timed(CtxGroup(ctxs), step)
+    torch.cuda.synchronize()
+    ctx = ctxs[(it[0] - 1) % depth]          # the context of the last step
     T_gpu, _, st_gpu = ctx.get_poses(n)      # fp64 poses of the last step
     lb = (it[0] - 1) & 1
     last_host = host[lb].numpy().reshape(-1, 4, 4)
@@ -351,6 +386,7 @@ def run_pairs(R):
         "global_pairs": n_glob, "pairs_per_gpu": n, "width": W, "height": H,
         "iters": a.iters, "fastdiv": ctx.fastdiv,
         "parallelism": f"dp{world} (contiguous pair shards, RCCL pose all-gather)",
+        "steps_in_flight": depth,
     }
     result["window_rates"] = [n_glob * a.steps / s for s in spread]
     result["roofline"] = roofline_icp(a, kt, n, W, H)
@@ -388,9 +424,10 @@ def run_pairs(R):
             leg["viewer_cloud"] = viewer_cloud_rate(R, d_dst[:64], dst[:64])
         if not a.no_spec_parity:
             leg["spec_parity"] = spec_parity(a, main)
-            leg["spec_parity"]["other_spec_rate"] = other_spec_rate(R, ctx, step, n_glob)
+            leg["spec_parity"]["other_spec_rate"] = other_spec_rate(R, ctxs, step, n_glob)
         result.update(leg)
-    ctx.close()
+    for c in ctxs:
+        c.close()
     return result
 
 
@@ -417,19 +454,23 @@ def gather_ms(R, local, out, world, counts, main, side, reps=5):
     return float(np.median(ts))
 
 
-def other_spec_rate(R, ctx, step, n_glob):
+def other_spec_rate(R, ctxs, step, n_glob):
     """The headline step in the OTHER spec a7/a8 arithmetic on the same
-    context and inputs (after the timed region): its rate and k_icp time."""
+    contexts and inputs (after the timed region): its rate and k_icp time."""
     a = R.a
     other = "fma" if a.spec == "survey" else "survey"
-    ctx.spec = other
+    torch.cuda.synchronize()
+    for c in ctxs:
+        c.spec = other
     for _ in range(5):
         step()
-    ctx.set_timing(True, iteration_kernel_only=True)
+    g = CtxGroup(ctxs)
+    g.set_timing(True, iteration_kernel_only=True)
     el = R.window(step, a.steps)
-    ms, n = ctx.get_timing(0)
-    ctx.set_timing(False)
-    ctx.spec = a.spec
+    ms, n = g.get_timing(0)
+    g.set_timing(False)
+    for c in ctxs:
+        c.spec = a.spec
     return {"spec": other, "value": n_glob * a.steps / el, "unit": "aligns/s",
             "k_icp_ms": ms / max(n, 1)}
 

@@ -79,7 +79,11 @@ constexpr int kPieces = kPartStride / 2;  // 16-byte pieces per row
 constexpr int kSumCols = 16;              // kSumCols * kPieces <= kRedThreads
 // Persistent-queue words (unsigned index into ctx->d_head), one 128-B line
 // apart so the contended dequeue atomic shares no line with the polled flag.
-constexpr int kQHead = 0, kQError = 32, kQSpins = 64, kQWaited = 96, kQWords = 128;
+// k_icp's work queues: up to kMaxQueues heads, kQHeads + 32 q (queue q holds
+// the pairs p = q (mod n_queues)).
+constexpr int kQHead = 0, kQError = 32, kQSpins = 64, kQWaited = 96, kQHeads = 128;
+constexpr int kMaxQueues = 8, kQHeadStride = 32;
+constexpr int kQWords = kQHeads + kMaxQueues * kQHeadStride;
 
 typedef float f4v __attribute__((ext_vector_type(4)));  // a gathered {z, nx, ny, nz} record
 typedef unsigned u4v __attribute__((ext_vector_type(4)));  // two doubles, raw bits
@@ -620,11 +624,14 @@ struct InitArgs {
 __device__ __forceinline__ void init_pairs(const InitArgs& ia, int tx, int ty, int f, int n_frames)
 {
     if (tx != 0 || ty != 0) return;
-    if (f == 0 && threadIdx.x == 0 && ia.head_err) {
-        ia.head_err[kQHead] = 0u;
-        ia.head_err[kQError] = 0u;
-        ia.head_err[kQSpins] = 0u;
-        ia.head_err[kQWaited] = 0u;
+    if (f == 0 && threadIdx.x < kMaxQueues && ia.head_err) {
+        if (threadIdx.x == 0) {
+            ia.head_err[kQHead] = 0u;
+            ia.head_err[kQError] = 0u;
+            ia.head_err[kQSpins] = 0u;
+            ia.head_err[kQWaited] = 0u;
+        }
+        ia.head_err[kQHeads + kQHeadStride * threadIdx.x] = 0u;  // queue heads
     }
     const int t = threadIdx.x;
     for (int p = f; p < ia.n; p += n_frames) {
@@ -1018,6 +1025,7 @@ __global__ void k_init(const double* __restrict__ T_init, int n, double* T64, fl
         head_err[kQError] = 0u;    // timeout flag (polled by waiters)
         head_err[kQSpins] = 0u;    // epoch polls (scheduler telemetry)
         head_err[kQWaited] = 0u;   // items that had to wait for their pair's pose
+        for (int q = 0; q < kMaxQueues; ++q) head_err[kQHeads + kQHeadStride * q] = 0u;
     }
     if (p >= n) return;
     for (int i = 0; i < 16; ++i) {
@@ -1528,11 +1536,43 @@ struct IterState {
     double* stats;        // [pair][iters][2] or null
     unsigned* arrivals;   // [pair][iters], zeroed per call
     unsigned* epoch;      // [pair], zeroed per call
-    unsigned* head;       // dequeue counter, zeroed per call
+    unsigned* head;       // queue words (telemetry at kQSpins / kQWaited), zeroed per call
     unsigned* error;      // timeout flag, zeroed per call
     float* T_out;         // [pair][16] fp32 4x4 written by the final solve, or null
     int iters, n_pairs, nblk, chunk;
+    int nq;               // work queues (1..kMaxQueues): heads at head[kQHeads + 32 q]
 };
+
+// One dequeue: from the workgroup's current queue q, moving on to the next
+// queue when q is drained (each queue holds the pairs p = q (mod nq), items
+// (iteration, pair, chunk) in that order).  Returns the item in the global
+// numbering item = (k n_pairs + p) nblk + c, or `total` when every queue is
+// drained.  Dependencies stay inside a queue (an item waits only on earlier
+// items of its own pairs, dequeued before it by running workgroups), so
+// every queue is deadlock-free on its own, as the single queue was; nq > 1
+// spreads the contended returning atomics over nq words (one per 128-B line):
+// MI355X_MICROARCH.md "dequeue": one head word pulled by 256+ CUs costs
+// ~3 us per dequeue, 8 per-XCD heads ~1.2 us.
+__device__ __forceinline__ int icp_dequeue(const IterState& is, int& q, int total)
+{
+    for (int v = 0; v < is.nq; ++v) {
+        const int npq = (is.n_pairs - q + is.nq - 1) / is.nq;
+        if (npq > 0) {
+            const int per = npq * is.nblk;
+            const int i = (int)__hip_atomic_fetch_add(is.head + (kQHeads - kQHead) + q * kQHeadStride,
+                                                      1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (i < is.iters * per) {
+                const int k = i / per;
+                const int rem = i - k * per;
+                const int pl = rem / is.nblk;
+                const int c = rem - pl * is.nblk;
+                return (k * is.n_pairs + q + is.nq * pl) * is.nblk + c;
+            }
+        }
+        q = q + 1 == is.nq ? 0 : q + 1;
+    }
+    return total;
+}
 
 constexpr unsigned kSpinMax = 1u << 23;  // x s_sleep(8) ~ seconds: a bound, never reached
 
@@ -1627,11 +1667,11 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
 
-    if (threadIdx.x == 0) {
-        const int first = (int)__hip_atomic_fetch_add(is.head, 1u, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT);
-        sh_item = icp_claim(is, first, total, per_iter, sh_T);
-    }
+    // thread 0's current queue: workgroups are dealt to the queues
+    // round-robin (b and b + 8 share an XCD, so with 8 queues each XCD pulls
+    // from its own head)
+    int myq = (int)(blockIdx.x % (unsigned)is.nq);
+    if (threadIdx.x == 0) sh_item = icp_claim(is, icp_dequeue(is, myq, total), total, per_iter, sh_T);
     __syncthreads();
     for (;;) {
         // LDS-broadcast values are wave-uniform: readfirstlane keeps them
@@ -1721,11 +1761,8 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
             }
         }
         // ---- next item (this workgroup has published: waiting is safe)
-        if (threadIdx.x == 0) {
-            const int next = (int)__hip_atomic_fetch_add(is.head, 1u, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT);
-            sh_item = icp_claim(is, next, total, per_iter, sh_T);
-        }
+        if (threadIdx.x == 0)
+            sh_item = icp_claim(is, icp_dequeue(is, myq, total), total, per_iter, sh_T);
         __syncthreads();
     }
 }
@@ -2221,6 +2258,7 @@ struct youth_icp_ctx {
     int track_ref = -1;  // ring slot (0/1) of the tracker's reference frame
     double* coop_res_host = nullptr;  // set around a tracker align: k_icp_coop writes its result there
     bool coop_tile_src = true;        // YOUTH_ICP_COOP_TILE_SRC=0: contiguous source chunks
+    int queues = kMaxQueues;         // k_icp work queues (YOUTH_ICP_QUEUES=1..8)
     int prep_xcd_map = 0;             // YOUTH_ICP_PREP_XCD_MAP=1: k_prep tiles contiguous per XCD (slower)
     // pipelined tracking (youth_icp_track_submit / _collect): up to
     // kTrackDepth frames in flight, each with a pinned staging buffer, pinned
@@ -2707,7 +2745,7 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
         const IterState is{c->d_T64,  c->d_T32,  c->d_status, c->d_stats,
                            c->d_arr_it, c->d_epoch, c->d_head + kQHead, c->d_head + kQError,
                            d_T_out,   iters,      n_pairs,    nb,
-                           chunk};
+                           chunk,     c->queues};
         if (exported) *exported = d_T_out != nullptr;  // k_icp's final solves write d_T_out
         const float thr2 = c->prm.dist_thresh * c->prm.dist_thresh;
         EventPair ep{};
@@ -2981,6 +3019,8 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         // persistent fallback of run_iterations
         const char* crf = getenv("YOUTH_ICP_TEST_REFUSE_COOP");
         c->coop_refuse = crf && *crf && *crf != '0';
+        const char* nqs = getenv("YOUTH_ICP_QUEUES");
+        if (nqs && atoi(nqs) >= 1 && atoi(nqs) <= kMaxQueues) c->queues = atoi(nqs);
         const char* pxm = getenv("YOUTH_ICP_PREP_XCD_MAP");
         if (pxm && (*pxm == '1' || *pxm == '2')) c->prep_xcd_map = *pxm - '0';
         const char* cts = getenv("YOUTH_ICP_COOP_TILE_SRC");
