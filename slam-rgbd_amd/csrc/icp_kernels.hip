@@ -2258,7 +2258,7 @@ struct youth_icp_ctx {
     int track_ref = -1;  // ring slot (0/1) of the tracker's reference frame
     double* coop_res_host = nullptr;  // set around a tracker align: k_icp_coop writes its result there
     bool coop_tile_src = true;        // YOUTH_ICP_COOP_TILE_SRC=0: contiguous source chunks
-    int queues = kMaxQueues;         // k_icp work queues (YOUTH_ICP_QUEUES=1..8)
+    int queues = 0;                  // k_icp work queues (YOUTH_ICP_QUEUES=1..8; 0: by batch size)
     int prep_xcd_map = 0;             // YOUTH_ICP_PREP_XCD_MAP=1: k_prep tiles contiguous per XCD (slower)
     // pipelined tracking (youth_icp_track_submit / _collect): up to
     // kTrackDepth frames in flight, each with a pinned staging buffer, pinned
@@ -2745,7 +2745,10 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
         const IterState is{c->d_T64,  c->d_T32,  c->d_status, c->d_stats,
                            c->d_arr_it, c->d_epoch, c->d_head + kQHead, c->d_head + kQError,
                            d_T_out,   iters,      n_pairs,    nb,
-                           chunk,     c->queues};
+                           chunk,
+                           // 8 per-XCD heads from 128 pairs (+0.7 % there), one below (64
+                           // pairs: -0.8 % with 8; profiles/r03/ab_queues.txt)
+                           c->queues ? c->queues : (n_pairs >= 128 ? kMaxQueues : 1)};
         if (exported) *exported = d_T_out != nullptr;  // k_icp's final solves write d_T_out
         const float thr2 = c->prm.dist_thresh * c->prm.dist_thresh;
         EventPair ep{};
