@@ -329,20 +329,48 @@ int youth_icp_track_frame(youth_icp_ctx* ctx, const int16_t* depth,
  * stream and its align (against the frame submitted before it) on the
  * context's stream, and returns without waiting, so the next frame's copy
  * overlaps the aligns in flight.  At most YOUTH_TRACK_MAX_IN_FLIGHT frames
- * may be in flight (YOUTH_EINVAL otherwise); with 3 in flight the next
- * frame's host copy and H2D hide behind two aligns.  youth_icp_track_collect waits for the OLDEST
+ * may be in flight (YOUTH_EINVAL otherwise): two suffice one frame at a
+ * time; two micro-batches of two (youth_icp_track_submit_batch) use four.  youth_icp_track_collect waits for the OLDEST
  * submitted frame and returns exactly what youth_icp_track_frame would have
  * returned for it (status bits or a negative code, T_rel, *has_ref).
  * youth_icp_track_frame = submit + collect, with nothing in flight. */
-#define YOUTH_TRACK_MAX_IN_FLIGHT 3
+#define YOUTH_TRACK_MAX_IN_FLIGHT 4
 int youth_icp_track_submit(youth_icp_ctx* ctx, const int16_t* depth,
                            const double* T_init);
 int youth_icp_track_collect(youth_icp_ctx* ctx, double* T_rel, int* has_ref);
 /* Frames submitted and not yet collected (0 .. YOUTH_TRACK_MAX_IN_FLIGHT). */
 int youth_icp_track_pending(const youth_icp_ctx* ctx);
 
+/* Micro-batch of n_frames consecutive host frames ([n_frames][H][W]) for a
+ * backlogged stream: the same as n_frames youth_icp_track_submit calls
+ * (T_init identity), each frame collected by its own youth_icp_track_collect
+ * with exactly the result youth_icp_track_frame gives, bit for bit.  When the
+ * context holds a reference and has room (max_frames >= 4), the frames are
+ * aligned by ONE cooperative launch in which pair i (frame i against frame
+ * i - 1, frame -1 = the reference) runs on the single-pair plan and waits
+ * for the pair before it to have prepped its target, if that grid fits
+ * (youth_icp_track_set_batch's plan: it does; the default one at
+ * 640x480 holds one pair); otherwise one launch per frame.  1 <= n_frames <= YOUTH_TRACK_MAX_BATCH, and at most
+ * YOUTH_TRACK_MAX_IN_FLIGHT frames in flight afterwards (EINVAL). */
+#define YOUTH_TRACK_MAX_BATCH 2
+int youth_icp_track_submit_batch(youth_icp_ctx* ctx, const int16_t* depth, int n_frames);
+
+/* Frames per submission youth_icp_track_host_sequence uses (1, default: one
+ * launch per frame; up to YOUTH_TRACK_MAX_BATCH: micro-batches).  Batch mode
+ * (> 1) plans the context's cooperative launches with the fewest source
+ * pixels per lane that let that many pairs share one grid (640x480: 5 px
+ * per lane, 120 workgroups per pair), so results stay bit-identical between
+ * batched and per-frame submission on that context (and within 1e-13 of the
+ * oracle, like the default plan).
+ * Returns the previous value or YOUTH_EINVAL. */
+int youth_icp_track_set_batch(youth_icp_ctx* ctx, int frames);
+/* Micro-batch launches this context has run (a batch that did not fit one
+ * grid runs as per-frame launches and is not counted). */
+long long youth_icp_track_chained(const youth_icp_ctx* ctx);
+
 /* A recorded host sequence (frames [n_frames][H][W], e.g. a .bin playback)
- * through the tracker, two frames in flight: the same results as
+ * through the tracker, two frames in flight (with youth_icp_track_set_batch(2):
+ * two micro-batches of two): the same results as
  * youth_icp_track_frame on each frame in order (continuing from the
  * reference the context holds).  T_rel [n][16] and status [n] (nullable)
  * receive the frames that had a reference, in order; returns how many, or a

@@ -63,7 +63,8 @@ constexpr int kTileW = 64;
 constexpr int kTileH = 48;
 constexpr int kPrepThreads = 512;
 // frames in flight through youth_icp_track_submit (YOUTH_TRACK_MAX_IN_FLIGHT):
-// with 3, frame k+1's host copy and H2D overlap frames k-1 and k's aligns
+// two one at a time, or two micro-batches of two, so the next submission's
+// host copy and H2D overlap the launch before it
 constexpr int kTrackDepth = YOUTH_TRACK_MAX_IN_FLIGHT;
 constexpr int kLdsW = kTileW + 2;
 constexpr int kLdsH = kTileH + 2;
@@ -1805,6 +1806,7 @@ constexpr int kCoopSetWords = kCoopPrepWords + kCoopMaxPairs * kCoopShardStride;
 constexpr int kCoopTileH = 24;  // fused prep tiles: 64 x 24 pixels (one per workgroup of a 640x480 pair: 200 tiles, G = 200)
 constexpr int kCoopTileHTall = 80;  // 64 x 80 (= 10 px per lane x 512: one per workgroup of a 1280x960 pair, G = 240)
 constexpr unsigned kCoopSpinMax = 1u << 22;  // polls (~1 us each): seconds, never reached
+constexpr int kCoopMaxChain = YOUTH_TRACK_MAX_BATCH;  // frames per tracker micro-batch
 
 struct CoopState {
     const double* T_init;  // [pair][16] or null (identity)
@@ -1830,6 +1832,15 @@ struct CoopState {
     // = npx x kThreads pixels), the tile it preps, so its iteration-0 gathers
     // (small motion) hit records it has just written; 0: a contiguous run
     int tile_src;
+    // tracker micro-batch (chain = 1; youth_icp_track_submit_batch): pairs
+    // (f_{p-1}, f_p) of consecutive frames.  Pair p preps its own source
+    // frame f_p into record frame prep_slot[p]; its target records are record
+    // frame tgt_slot[p]: pair 0 the reference, pair p >= 1 the frame pair p-1
+    // preps in this launch, so pair p waits for pair p-1's prep counter.
+    // Pair p's result goes to the pinned slot res_pair[p].
+    int chain;
+    int tgt_slot[kCoopMaxChain], prep_slot[kCoopMaxChain];
+    double* res_pair[kCoopMaxChain];
 };
 
 // Phase timestamps for tools/coopbench only (never in the product build):
@@ -1928,6 +1939,11 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
     unsigned* cnt = cs.set + (size_t)p * kCoopShards * kCoopShardStride;
     unsigned* err = cs.set + kCoopErrWord;
     unsigned* prep_cnt = cs.set + kCoopPrepWords + (size_t)p * kCoopShardStride;
+    // the prep counter this pair waits on: its own (prep_wait), or in a
+    // tracker chain the previous pair's (whose prep is this pair's target)
+    const bool prep_wait = cs.chain ? p > 0 : cs.prep_wait != 0;
+    unsigned* wait_cnt = cs.chain ? prep_cnt - kCoopShardStride : prep_cnt;
+    const int tgt_frame = cs.chain ? cs.tgt_slot[p] : pm.tgt0 + p;
     float* X = coop_src;
     float* Y = coop_src + npx * kThreads;
     float* Z = coop_src + 2 * npx * kThreads;
@@ -1954,7 +1970,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
         const int tiles_x = (W + kTileW - 1) / kTileW;
         const int tiles = tiles_x * ((H + kTH - 1) / kTH);
         const int16_t* tdep = cs.prep_src + (size_t)p * N;
-        float4* R = const_cast<float4*>(recs) + (size_t)(cs.prep_out0 + p) * P;
+        float4* R = const_cast<float4*>(recs) +
+                    (size_t)(cs.chain ? cs.prep_slot[p] : cs.prep_out0 + p) * P;
         for (int t = c; t < tiles; t += G) {  // uniform per workgroup
             const int ty = t / tiles_x;
             const int x0 = (t - ty * tiles_x) * kTileW, y0 = ty * kTH;
@@ -1968,7 +1985,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
         __syncthreads();
-        if (cs.prep_wait && threadIdx.x == 0)
+        if ((cs.prep_wait || cs.chain) && threadIdx.x == 0)
             __hip_atomic_fetch_add(prep_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     COOP_MARK(0, 15);  // prep published
@@ -2002,7 +2019,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
         }
     }
     const __amdgpu_buffer_rsrc_t rrec = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float4*>(recs + (size_t)(pm.tgt0 + p) * P), (short)0,
+        const_cast<float4*>(recs + (size_t)tgt_frame * P), (short)0,
         (int)(P * sizeof(float4)), 0x00020000);
     // shard s of this pair holds (k+1) x n_s after iteration k
     const int my_shard = c & (kCoopShards - 1);
@@ -2011,13 +2028,13 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
     int32_t st_acc = 0;
     bool timeout = false;
     COOP_MARK(1, 15);  // source pixels staged
-    if (cs.prep_src && cs.prep_wait) {
+    if (cs.prep_src && prep_wait) {
         // every workgroup of pair p prepped its tiles: ONE relaxed poll, ONE
         // agent acquire (drops this CU's stale L1 lines), then plain gathers
         if (threadIdx.x == 0) {
             unsigned spins = 0;
             int stop = 0;
-            while (ld_u32_sc1(prep_cnt) < (unsigned)G) {
+            while (ld_u32_sc1(wait_cnt) < (unsigned)G) {
                 __builtin_amdgcn_s_sleep(1);
                 if (++spins > kCoopSpinMax || ld_u32_sc1(err) != 0u) {
                     __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2139,13 +2156,14 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
         if (cs.T_out) cs.T_out[(size_t)p * 16 + i] = i < 12 ? (float)v : (i == 15 ? 1.0f : 0.0f);
         const int32_t st = st_acc | (timeout ? YOUTH_STATUS_TIMEOUT : 0);
         if (i == 0) cs.status[p] = st;
-        if (cs.res_host && p == 0) {
+        double* res = cs.chain ? cs.res_pair[p] : (p == 0 ? cs.res_host : nullptr);
+        if (res) {
             // fine-grained pinned slot: system-scope stores go to host memory
             // past the L2, and the wave waits for them before it ends, so the
             // tracker's completion event needs no system-scope L2 writeback
-            __hip_atomic_store(cs.res_host + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(res + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             if (i == 0)
-                __hip_atomic_store(reinterpret_cast<int32_t*>(cs.res_host + 16), st,
+                __hip_atomic_store(reinterpret_cast<int32_t*>(res + 16), st,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __builtin_amdgcn_s_waitcnt(0);
         }
@@ -2239,11 +2257,13 @@ struct youth_icp_ctx {
     // small batches: k_icp_coop (youth_icp_create reads the knobs)
     bool coop = true;                // YOUTH_ICP_NO_COOP=1 disables
     int coop_px = 0;                 // YOUTH_ICP_COOP_PX: force pixels per lane (0: plan)
+    int coop_px_env = 0;             // coop_px outside the tracker's batch mode
     int coop_threads = 512;          // YOUTH_ICP_COOP_THREADS=256: one wave per SIMD
     int coop_max_pairs = kCoopMaxPairs;  // YOUTH_ICP_COOP_MAX_PAIRS (<= kCoopMaxPairs)
     int coop_launch = 0;             // YOUTH_ICP_COOP_LAUNCH: 0 serial (default), 1 runtime, 2 plain
     bool coop_refuse = false;        // YOUTH_ICP_TEST_REFUSE_COOP=1 (test hook)
-    int coop_bpc[4][kCoopMaxPx + 1] = {};  // occupancy of k_icp_coop<spec, fast> [spec 2 + fast] at npx (LDS)
+    // occupancy of k_icp_coop<spec, fast, threads> [threads 256?][spec 2 + fast] at npx (LDS)
+    int coop_bpc[2][4][kCoopMaxPx + 1] = {};
     int coop_bpc_tall[4] = {};              // the 64 x 80 prep-tile kernel at 10 px per lane
     unsigned* d_coop = nullptr;      // 2 counter sets of kCoopSetWords
     int32_t* d_status_out = nullptr; // [max_frames] host batch API: status per pair of the call
@@ -2258,6 +2278,8 @@ struct youth_icp_ctx {
     int track_ref = -1;  // ring slot (0/1) of the tracker's reference frame
     double* coop_res_host = nullptr;  // set around a tracker align: k_icp_coop writes its result there
     bool coop_tile_src = true;        // YOUTH_ICP_COOP_TILE_SRC=0: contiguous source chunks
+    int trk_batch = 1;                // frames per submission in youth_icp_track_host_sequence
+    long long trk_chained = 0;        // micro-batch launches so far (youth_icp_track_chained)
     int queues = 0;                  // k_icp work queues (YOUTH_ICP_QUEUES=1..8; 0: by batch size)
     int prep_xcd_map = 0;             // YOUTH_ICP_PREP_XCD_MAP=1: k_prep tiles contiguous per XCD (slower)
     // pipelined tracking (youth_icp_track_submit / _collect): up to
@@ -2273,7 +2295,8 @@ struct youth_icp_ctx {
         hipEvent_t ev = nullptr;       // the one of the two recorded for this submission
         int has_ref = 0;
     } trk[kTrackDepth];
-    int trk_slot_last[2] = {-1, -1};  // trk[] entry of the last align that read depth slot d
+    int trk_dslot_last[4] = {-1, -1, -1, -1};  // trk[] entry of the last launch that read depth slot d
+    int trk_prev_d0 = -1;                       // first depth slot of the last launch
     int trk_head = 0, trk_n = 0;       // oldest in-flight submission, count in flight
 
     // host-buffer batch API: H2D of chunk k+1 on xfer overlaps the align of chunk k
@@ -2504,7 +2527,7 @@ static bool coop_plan(const youth_icp_ctx* c, int n_pairs, int* npx_out, int* G_
         // VGPR-limited occupancy: k_icp_coop's SGPR count (106) admits 6
         // 256-thread blocks per CU (MI355X_MICROARCH.md residency formula),
         // more than the API's VGPR answer, so the API count is exact here
-        const int bpc = c->coop_bpc[v][npx];
+        const int bpc = c->coop_bpc[c->coop_threads == 256][v][npx];
         if (bpc < 1 || wgs > (long long)c->n_cu * bpc) continue;
         const long long cost = (long long)npx * ((wgs + c->n_cu - 1) / c->n_cu);
         if (best < 0 || cost <= best) {
@@ -2542,6 +2565,12 @@ struct PrepJob {
     const int16_t* depth;
     int n, out0;
     bool wait;
+    // tracker micro-batch (k_icp_coop only; CoopState.chain): pair p preps
+    // its source frame into record frame prep_slot[p] and gathers record
+    // frame tgt_slot[p]; results to the pinned slots res[p]
+    bool chain = false;
+    int tgt_slot[kCoopMaxChain] = {}, prep_slot[kCoopMaxChain] = {};
+    double* res[kCoopMaxChain] = {};
 };
 
 // k_icp_coop's workgroups poll each other, so all n_pairs x G of them must be
@@ -2635,6 +2664,14 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
                  n_pairs,  G,        npx,      job ? job->depth : nullptr,
                  job ? job->out0 : 0, job && job->wait ? 1 : 0, wide ? 1 : 0,
                  c->coop_res_host, tile_src ? 1 : 0};
+    if (job && job->chain) {
+        cs.chain = 1;
+        for (int i = 0; i < kCoopMaxChain; ++i) {
+            cs.tgt_slot[i] = job->tgt_slot[i];
+            cs.prep_slot[i] = job->prep_slot[i];
+            cs.res_pair[i] = job->res[i];
+        }
+    }
     const float4* recs = c->d_rec;
     size_t P = c->P;
     int W = c->W, H = c->H;
@@ -2679,8 +2716,23 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
     // k_icp_coop fuses the prep job (one pair of workgroups per target);
     // every other path runs k_prep first
     int npx = 0, G = 0;
-    const bool coop = iters > 0 && (!job || job->n == n_pairs || (!job->wait && job->n == 1)) &&
-                      coop_plan(c, n_pairs, &npx, &G);
+    bool coop;
+    if (job && job->chain) {
+        // a tracker micro-batch runs every pair on the single-pair plan, so
+        // each pair's summation tree (and pose) is the one track_frame gives;
+        // refused (EINVAL, nothing enqueued) when that grid is not co-resident
+        if (iters <= 0 || job->n != n_pairs || n_pairs > kCoopMaxChain ||
+            !coop_plan(c, 1, &npx, &G) ||
+            (long long)n_pairs * G >
+                (long long)c->n_cu *
+                    c->coop_bpc[c->coop_threads == 256][c->spec * 2 + (c->fast ? 1 : 0)][npx])
+            return set_error(YOUTH_EINVAL, "track batch: %d pairs do not fit one cooperative grid",
+                             n_pairs);
+        coop = true;
+    } else {
+        coop = iters > 0 && (!job || job->n == n_pairs || (!job->wait && job->n == 1)) &&
+               coop_plan(c, n_pairs, &npx, &G);
+    }
     c->last_coop = coop;
     int rc = ensure_stats(c, iters > 0 ? iters : 1);
     if (rc) return rc;
@@ -2705,6 +2757,7 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
             c->last_stream = s;
             return YOUTH_OK;
         }
+        if (job && job->chain) return rc;  // a micro-batch has no other kernel path
         // the runtime refused the cooperative launch (nothing was enqueued): this
         // context takes the persistent path from now on
         fprintf(stderr, "youth_icp: cooperative launch refused (%s); using the persistent path\n",
@@ -2993,15 +3046,17 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         c->persistent = !(np && *np && *np != '0');
         const char* cth = getenv("YOUTH_ICP_COOP_THREADS");
         if (cth && atoi(cth) == 256) c->coop_threads = 256;
-        for (int v = 0; v < 4; ++v)
-            for (int npx = 1; npx <= kCoopMaxPx; ++npx) {
-                int nb = 0;
-                if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                         &nb, coop_kernel(v >> 1, (v & 1) != 0, c->coop_threads), c->coop_threads,
-                         coop_lds(npx, c->coop_threads))) != hipSuccess)
-                    return fail("occupancy coop", e);
-                c->coop_bpc[v][npx] = nb;
-            }
+        for (int ti = 0; ti < 2; ++ti)
+            for (int v = 0; v < 4; ++v)
+                for (int npx = 1; npx <= kCoopMaxPx; ++npx) {
+                    const int th = ti ? 256 : 512;
+                    int nb = 0;
+                    if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                             &nb, coop_kernel(v >> 1, (v & 1) != 0, th), th, coop_lds(npx, th))) !=
+                        hipSuccess)
+                        return fail("occupancy coop", e);
+                    c->coop_bpc[ti][v][npx] = nb;
+                }
         for (int v = 0; v < 4; ++v) {
             int nb = 0;
             const int npx = kTileW * kCoopTileHTall / 512;
@@ -3015,6 +3070,7 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         c->coop = !(nc && *nc && *nc != '0');
         const char* cpx = getenv("YOUTH_ICP_COOP_PX");
         if (cpx && atoi(cpx) >= 1 && atoi(cpx) <= kCoopMaxPx) c->coop_px = atoi(cpx);
+        c->coop_px_env = c->coop_px;
         const char* cl = getenv("YOUTH_ICP_COOP_LAUNCH");
         c->coop_launch = !cl ? 0 : strcmp(cl, "runtime") == 0 ? 1 : strcmp(cl, "plain") == 0 ? 2 : 0;
         // test hook (tests/test_gpu_parity.py): every cooperative launch of
@@ -3582,6 +3638,123 @@ static int ensure_track(youth_icp_ctx* c)
     return YOUTH_OK;
 }
 
+// Depth slots of the tracker (device staging of host frames): 4 when the
+// context has room (a micro-batch takes two consecutive ones, the other half
+// stays with the launch before), else 2.  Record slots: 3 (a micro-batch
+// preps two new frames beside the reference), else 2.
+static int trk_depth_slots(const youth_icp_ctx* c) { return c->max_frames >= 4 ? 4 : 2; }
+static int trk_record_slots(const youth_icp_ctx* c) { return c->max_frames >= 3 ? 3 : 2; }
+
+// Whether m consecutive frames can be aligned as one k_icp_coop micro-batch:
+// every pair on the single-pair plan (bit-identical to track_frame), the m
+// grids co-resident, room for the slots.
+static bool trk_chain_fits(const youth_icp_ctx* c, int m)
+{
+    if (m < 2 || m > kCoopMaxChain || trk_depth_slots(c) < 2 * m || trk_record_slots(c) < m + 1 ||
+        c->prm.iters <= 0 || c->coop_refuse)
+        return false;
+    int npx = 0, G = 0;
+    if (!coop_plan(c, 1, &npx, &G)) return false;
+    return (long long)m * G <=
+           (long long)c->n_cu *
+               c->coop_bpc[c->coop_threads == 256][c->spec * 2 + (c->fast ? 1 : 0)][npx];
+}
+
+// m consecutive host frames (m = 1, or a micro-batch that trk_chain_fits):
+// staged into m consecutive depth slots not read by the previous launch,
+// H2D on the transfer stream (after the last launch that read those slots),
+// then ONE launch on the context stream: prep only (no reference yet), the
+// single-pair align with the fused prep of the new frame, or the chained
+// micro-batch (pair i aligns frame i to frame i-1, frame -1 = the
+// reference).  One completion event for the launch, shared by its entries.
+static int track_submit_frames(youth_icp_ctx* c, const int16_t* depth, int m,
+                               const double* T_init)
+{
+    hipStream_t s = c->stream;
+    const size_t N = c->N;
+    const int nds = trk_depth_slots(c), nrs = trk_record_slots(c);
+    // depth slots: the half (or slot) the previous launch did not use
+    int d0;
+    if (nds == 4)
+        d0 = c->trk_prev_d0 >= 2 || c->trk_prev_d0 < 0 ? 0 : 2;
+    else
+        d0 = c->trk_prev_d0 == 0 ? 1 : 0;
+    // record slots for the new frames: the first m that are not the reference
+    const int ref = c->track_ref;
+    int rs[kCoopMaxChain] = {0, 0};
+    for (int r = 0, k = 0; r < nrs && k < m; ++r)
+        if (r != ref) rs[k++] = r;
+    int qi[kCoopMaxChain];
+    for (int i = 0; i < m; ++i) qi[i] = (c->trk_head + c->trk_n + i) % kTrackDepth;
+    auto& ql = c->trk[qi[m - 1]];
+    // the caller's buffers are free on return: copy into the entries' pinned
+    // staging, then H2D after the last launch that read these depth slots
+    for (int i = 0; i < m; ++i) {
+        memcpy(c->trk[qi[i]].pinned, depth + (size_t)i * N, N * sizeof(int16_t));
+        const int last = c->trk_dslot_last[d0 + i];
+        if (last >= 0) HIP_TRY(hipStreamWaitEvent(c->xfer, c->trk[last].ev, 0));
+    }
+    for (int i = 0; i < m; ++i)
+        HIP_TRY(hipMemcpyAsync(c->d_depth + (size_t)(d0 + i) * N, c->trk[qi[i]].pinned,
+                               N * sizeof(int16_t), hipMemcpyHostToDevice, c->xfer));
+    HIP_TRY(hipEventRecord(ql.h2d, c->xfer));
+    HIP_TRY(hipStreamWaitEvent(s, ql.h2d, 0));
+    const int16_t* dsrc = c->d_depth + (size_t)d0 * N;
+    int rc = YOUTH_OK;
+    bool kernel_result = false;  // k_icp_coop stored the result(s) to host memory
+    if (ref < 0) {
+        // first frame of a sequence: prep only (m == 1)
+        rc = launch_prep(c, s, dsrc, 1, rs[0], false);
+    } else if (m == 1) {
+        // source: the new frame's depth; target: ref's records; the new frame
+        // is prepped beside the iterations as the next reference.  k_icp_coop
+        // writes the result into the pinned slot itself; any other kernel path
+        // copies it
+        const PrepJob job{dsrc, 1, rs[0], false};
+        c->coop_res_host = ql.res;
+        rc = run_iterations(c, s, dsrc, PairMap{0, ref}, 1, T_init, nullptr, nullptr, &job);
+        c->coop_res_host = nullptr;
+        kernel_result = c->last_coop;
+        if (rc == YOUTH_OK && !c->last_coop) {
+            HIP_TRY(hipMemcpyAsync(ql.res, c->d_T64, 16 * sizeof(double), hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipMemcpyAsync(ql.res + 16, c->d_status, sizeof(int32_t),
+                                   hipMemcpyDeviceToHost, s));
+        }
+    } else {
+        PrepJob job{dsrc, m, 0, false};
+        job.chain = true;
+        for (int i = 0; i < m; ++i) {
+            job.tgt_slot[i] = i == 0 ? ref : rs[i - 1];
+            job.prep_slot[i] = rs[i];
+            job.res[i] = c->trk[qi[i]].res;
+        }
+        rc = run_iterations(c, s, dsrc, PairMap{0, 0}, m, nullptr, nullptr, nullptr, &job);
+        kernel_result = true;
+        if (rc == YOUTH_OK) ++c->trk_chained;
+    }
+    if (rc) {
+        // nothing of these frames is kept; wait for what was enqueued so the
+        // staging buffers and the slots are not in use by dropped frames
+        (void)hipStreamSynchronize(s);
+        (void)hipStreamSynchronize(c->xfer);
+        return rc;
+    }
+    // no result to publish (first frame) or k_icp_coop stored it to host
+    // memory itself: no system-scope fence; else the copies' result needs it
+    hipEvent_t ev = (ref < 0 || kernel_result) ? ql.done_nf : ql.done;
+    HIP_TRY(hipEventRecord(ev, s));
+    for (int i = 0; i < m; ++i) {
+        auto& q = c->trk[qi[i]];
+        q.ev = ev;
+        q.has_ref = (i > 0 || ref >= 0) ? 1 : 0;
+        c->trk_dslot_last[d0 + i] = qi[m - 1];
+    }
+    c->trk_prev_d0 = d0;
+    c->track_ref = rs[m - 1];
+    c->trk_n += m;
+    return YOUTH_OK;
+}
+
 int youth_icp_track_submit(youth_icp_ctx* c, const int16_t* depth, const double* T_init)
 {
     if (!c || !depth) return set_error(YOUTH_EINVAL, "track_submit: bad arguments");
@@ -3596,57 +3769,34 @@ int youth_icp_track_submit(youth_icp_ctx* c, const int16_t* depth, const double*
     if (rc) return rc;
     rc = ensure_track(c);
     if (rc) return rc;
-    hipStream_t s = c->stream;
+    return track_submit_frames(c, depth, 1, T_init);
+}
+
+int youth_icp_track_submit_batch(youth_icp_ctx* c, const int16_t* depth, int n_frames)
+{
+    if (!c || !depth || n_frames < 1 || n_frames > YOUTH_TRACK_MAX_BATCH)
+        return set_error(YOUTH_EINVAL, "track_submit_batch: bad arguments (%d frames)", n_frames);
+    if (c->trk_n + n_frames > kTrackDepth)
+        return set_error(YOUTH_EINVAL, "track_submit_batch: %d + %d frames in flight (max %d)",
+                         c->trk_n, n_frames, kTrackDepth);
+    int rc = bind_device(c);
+    if (rc) return rc;
+    rc = ensure_track(c);
+    if (rc) return rc;
     const size_t N = c->N;
-    const int qi = (c->trk_head + c->trk_n) % kTrackDepth;
-    auto& q = c->trk[qi];
-    // the new frame goes to the ring slot that is not the reference; its depth
-    // was last read (as a source) by the align two submissions back
-    const int slot = c->track_ref == 0 ? 1 : 0;
-    memcpy(q.pinned, depth, N * sizeof(int16_t));  // the caller's buffer is free on return
-    // (that align's `done` event: one event record per frame, ~3 us each on
-    // the stream; profiles/r02/event_gap_s53.txt)
-    if (c->trk_slot_last[slot] >= 0)
-        HIP_TRY(hipStreamWaitEvent(c->xfer, c->trk[c->trk_slot_last[slot]].ev, 0));
-    HIP_TRY(hipMemcpyAsync(c->d_depth + (size_t)slot * N, q.pinned, N * sizeof(int16_t),
-                           hipMemcpyHostToDevice, c->xfer));
-    HIP_TRY(hipEventRecord(q.h2d, c->xfer));
-    HIP_TRY(hipStreamWaitEvent(s, q.h2d, 0));
-    // the new frame is the next submission's target: its records go to `slot`
-    // (beside this call's iterations, which gather ref's records)
-    const PrepJob job{c->d_depth + (size_t)slot * N, 1, slot, false};
-    const int ref = c->track_ref;
-    q.has_ref = ref >= 0;
-    if (ref < 0) {
-        rc = launch_prep(c, s, job.depth, 1, slot, false);
-    } else {
-        // source: the new frame's depth; target: ref's records.  k_icp_coop
-        // writes the result into the pinned slot itself (no copies on the
-        // stream); any other kernel path copies it
-        c->coop_res_host = q.res;
-        rc = run_iterations(c, s, c->d_depth + (size_t)slot * N, PairMap{0, ref}, 1, T_init,
-                            nullptr, nullptr, &job);
-        c->coop_res_host = nullptr;
-        if (rc == YOUTH_OK && !c->last_coop) {
-            HIP_TRY(hipMemcpyAsync(q.res, c->d_T64, 16 * sizeof(double), hipMemcpyDeviceToHost, s));
-            HIP_TRY(hipMemcpyAsync(q.res + 16, c->d_status, sizeof(int32_t),
-                                   hipMemcpyDeviceToHost, s));
-        }
+    int done = 0;
+    if (c->track_ref < 0) {  // no reference yet: the first frame is only prepped
+        rc = track_submit_frames(c, depth, 1, nullptr);
+        if (rc) return rc;
+        done = 1;
     }
-    if (rc) {
-        // nothing of this frame is kept; wait for what was enqueued so the
-        // staging buffer and the ring slot are not in use by a dropped frame
-        (void)hipStreamSynchronize(s);
-        (void)hipStreamSynchronize(c->xfer);
-        return rc;
+    const int rest = n_frames - done;
+    if (rest >= 2 && trk_chain_fits(c, rest))
+        return track_submit_frames(c, depth + (size_t)done * N, rest, nullptr);
+    for (int i = done; i < n_frames; ++i) {  // one launch per frame
+        rc = track_submit_frames(c, depth + (size_t)i * N, 1, nullptr);
+        if (rc) return rc;
     }
-    // no result to publish (first frame) or k_icp_coop stored it to host
-    // memory itself: no system-scope fence; else the copies' result needs it
-    q.ev = (ref < 0 || c->last_coop) ? q.done_nf : q.done;
-    HIP_TRY(hipEventRecord(q.ev, s));
-    c->trk_slot_last[slot] = qi;
-    c->track_ref = slot;
-    ++c->trk_n;
     return YOUTH_OK;
 }
 
@@ -3700,13 +3850,27 @@ int youth_icp_track_host_sequence(youth_icp_ctx* c, const int16_t* frames, int n
         }
         return YOUTH_OK;
     };
-    for (int f = 0; f < n_frames; ++f) {
-        int rc = youth_icp_track_submit(c, frames + (size_t)f * N, nullptr);
-        if (rc == YOUTH_OK && c->trk_n == 2) rc = collect();  // two in flight, as the worker
+    // batch: frames per submission (1: one launch per frame, as the SLAM
+    // worker at camera rate; 2: micro-batches of two frames when they fit one
+    // cooperative grid, the pose of each frame bit-identical either way)
+    const int batch = c->trk_batch;
+    for (int f = 0; f < n_frames;) {
+        const int m = std::min(batch, n_frames - f);
+        // keep two submissions in flight: two frames, or two micro-batches
+        while (c->trk_n + m > (batch > 1 ? 2 * batch : 2)) {
+            const int rc = collect();
+            if (rc) {
+                while (c->trk_n) (void)collect();
+                return rc;
+            }
+        }
+        const int rc = m == 1 ? youth_icp_track_submit(c, frames + (size_t)f * N, nullptr)
+                              : youth_icp_track_submit_batch(c, frames + (size_t)f * N, m);
         if (rc) {
             while (c->trk_n) (void)collect();
             return rc;
         }
+        f += m;
     }
     while (c->trk_n) {
         const int rc = collect();
@@ -3727,6 +3891,34 @@ int youth_icp_track_frame(youth_icp_ctx* c, const int16_t* depth, const double* 
     if (rc) return rc;
     return youth_icp_track_collect(c, T_rel, has_ref);
 }
+
+int youth_icp_track_set_batch(youth_icp_ctx* c, int frames)
+{
+    if (!c || frames < 1 || frames > YOUTH_TRACK_MAX_BATCH)
+        return set_error(YOUTH_EINVAL, "track_set_batch: bad arguments (%d)", frames);
+    const int old = c->trk_batch;
+    c->trk_batch = frames;
+    // batch mode: the fewest source pixels per lane whose workgroups for
+    // `frames` pairs fit one grid (512-thread workgroups at 221 VGPRs are one
+    // per CU: 256 per grid; 640x480: 5 px per lane, 120 workgroups per pair),
+    // for every coop launch of the context, so batched and per-frame
+    // submissions stay bit-identical
+    c->coop_px = c->coop_px_env;
+    if (frames > 1) {
+        const int v = c->spec * 2 + (c->fast ? 1 : 0);
+        for (int npx = 1; npx <= kCoopMaxPx; ++npx) {
+            const long long G = (c->N + (long long)npx * c->coop_threads - 1) /
+                                ((long long)npx * c->coop_threads);
+            if (frames * G <= (long long)c->n_cu * c->coop_bpc[c->coop_threads == 256][v][npx]) {
+                c->coop_px = npx;
+                break;
+            }
+        }
+    }
+    return old;
+}
+
+long long youth_icp_track_chained(const youth_icp_ctx* c) { return c ? c->trk_chained : 0; }
 
 void youth_icp_track_reset(youth_icp_ctx* c)
 {

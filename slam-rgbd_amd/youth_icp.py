@@ -127,6 +127,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "youth_icp_track_submit": (c_int, [c_void_p, P16, PD]),
         "youth_icp_track_collect": (c_int, [c_void_p, PD, POINTER(c_int)]),
         "youth_icp_track_pending": (c_int, [c_void_p]),
+        "youth_icp_track_submit_batch": (c_int, [c_void_p, P16, c_int]),
+        "youth_icp_track_set_batch": (c_int, [c_void_p, c_int]),
+        "youth_icp_track_chained": (ctypes.c_longlong, [c_void_p]),
         "youth_icp_track_host_sequence": (c_int, [c_void_p, P16, c_int, PD, POINTER(c_int32)]),
         "youth_parse_camera_yaml": (c_int, [c_char_p, POINTER(Intrinsics), POINTER(c_int),
                                             POINTER(c_int)]),
@@ -177,7 +180,8 @@ def _err(code: int) -> IcpError:
     return IcpError(code, (lib.youth_icp_last_error() or b"").decode())
 
 
-TRACK_MAX_IN_FLIGHT = 3   # YOUTH_TRACK_MAX_IN_FLIGHT (include/youth_icp.h)
+TRACK_MAX_IN_FLIGHT = 4   # YOUTH_TRACK_MAX_IN_FLIGHT (include/youth_icp.h)
+TRACK_MAX_BATCH = 2       # YOUTH_TRACK_MAX_BATCH
 
 
 def _check(code: int) -> int:
@@ -478,6 +482,21 @@ class IcpContext:
         st = _check(self._lib.youth_icp_track_collect(self._ctx, _p(T, c_double),
                                                       ctypes.byref(has)))
         return T, st, bool(has.value)
+
+    def track_submit_batch(self, frames: np.ndarray) -> None:
+        """Micro-batch of consecutive frames [m, H, W] (m <= TRACK_MAX_BATCH):
+        one cooperative launch when it fits, each frame then collected by its
+        own track_collect with track_frame's result bit for bit."""
+        f = np.ascontiguousarray(frames, np.int16).reshape(-1, self.H, self.W)
+        _check(self._lib.youth_icp_track_submit_batch(self._ctx, _p(f, c_int16), f.shape[0]))
+
+    def track_set_batch(self, frames: int) -> int:
+        """Frames per submission of track_host_sequence; returns the previous."""
+        return _check(self._lib.youth_icp_track_set_batch(self._ctx, frames))
+
+    def track_chained(self) -> int:
+        """Micro-batch launches run so far on this context."""
+        return int(self._lib.youth_icp_track_chained(self._ctx))
 
     def track_pending(self) -> int:
         return int(self._lib.youth_icp_track_pending(self._ctx))

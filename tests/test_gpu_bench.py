@@ -67,6 +67,8 @@ def test_bench_single_gpu_contract():
         assert rf3["unit"] == "GB/s" and 0 < rf3["frac"] < 1.0 and rf3["launches"] > 0
     assert d["c5"]["parity_ok"] and d["c5"]["batch"]["trajectory_frames"] == 41
     assert d["c5"]["streamed"]["max_abs_diff_vs_batch_poses"] <= 1e-5
+    assert d["c5"]["streamed"]["pipelined_equals_sync"]
+    assert d["c5"]["streamed"]["batched_equals_sync"]
     assert d["kernel_path"]["kernel"].startswith("k_prep + k_icp")
     assert d["viewer_cloud"]["bit_exact_vs_cpu"]
     # spec a7/a8: the default is SURVEY §8a as worded; both arithmetics

@@ -427,7 +427,7 @@ def test_track_submit_collect_pipelined():
         with pytest.raises(youth_icp.IcpError):
             ctx.track_collect()                              # nothing in flight
         got = []
-        order = "SCSSCCSSSCSCSCCSCC"   # S = submit next frame, C = collect oldest (<= 3 in flight)
+        order = "SCSSCCSSSCSCSCCSCC"   # S = submit next frame, C = collect oldest (<= 4 in flight)
         k = 0
         for op in order:
             if op == "S":
@@ -438,20 +438,21 @@ def test_track_submit_collect_pipelined():
         assert k == len(frames) and len(got) == len(frames) and ctx.track_pending() == 0
         for (Tg, sg, hg), (Tw, sw, hw) in zip(got, want):
             assert np.array_equal(Tg, Tw) and sg == sw and hg == hw
-        assert youth_icp.TRACK_MAX_IN_FLIGHT == 3
-        for f in range(3):
+        D = youth_icp.TRACK_MAX_IN_FLIGHT
+        assert D == 4
+        for f in range(D):
             ctx.track_submit(frames[f])
         with pytest.raises(youth_icp.IcpError):
-            ctx.track_submit(frames[3])                      # a fourth frame in flight
+            ctx.track_submit(frames[D])                      # one frame too many in flight
         with pytest.raises(youth_icp.IcpError):
-            ctx.track_frame(frames[3])                       # frames not collected
-        ctx.track_reset()                                    # frames 0, 1 and 2 in flight
+            ctx.track_frame(frames[D])                       # frames not collected
+        ctx.track_reset()                                    # frames 0 .. D-1 in flight
         _, _, h0 = ctx.track_collect()
-        ctx.track_submit(frames[3])
-        hs = [h0] + [ctx.track_collect()[2] for _ in range(3)]
-        assert hs == [True, True, True, False]               # frame 3 starts a new sequence
-        T, st, has = ctx.track_frame(frames[4])
-        T64, _, sto, _ = oracle.align(frames[4], frames[3])
+        ctx.track_submit(frames[D])
+        hs = [h0] + [ctx.track_collect()[2] for _ in range(D)]
+        assert hs == [True] * D + [False]                    # frame D starts a new sequence
+        T, st, has = ctx.track_frame(frames[D + 1])
+        T64, _, sto, _ = oracle.align(frames[D + 1], frames[D])
         assert has and st == sto and _pose_err(T, T64) <= POSE_TOL
         # the library's own loop over a host sequence: the same results
         ctx.track_reset()
@@ -883,3 +884,56 @@ def test_prep_tile_orders_bit_identical(xcd_map, monkeypatch):
             assert np.array_equal(_bits(a), _bits(b))
         assert np.array_equal(out["0"][1], out[xcd_map][1])
         assert np.array_equal(out["0"][2], out[xcd_map][2]) and not out["0"][2].any()
+
+
+def test_track_micro_batches_bit_identical():
+    """youth_icp_track_submit_batch: two consecutive frames aligned by ONE
+    k_icp_coop launch (pair 1 waits for pair 0's prep of its target), each
+    frame collected separately with exactly the result track_frame gives in
+    the same mode (pose bits, status, has_ref): the first frame of a
+    sequence, odd counts, singles between batches, a reset with a batch in
+    flight, the library loop in micro-batches; the default plan (one pair
+    per grid: per-frame launches) and the batch mode's plan (5 px per lane:
+    chained launches), both within 1e-5 of the oracle; a context too small
+    for batches falls back to per-frame launches."""
+    frames, _ = youth_synth.sequence(5, 12)
+    for batch_mode, max_frames in ((False, 4), (True, 4), (True, 2)):
+        with youth_icp.IcpContext(640, 480, 4) as ref:
+            if batch_mode:
+                ref.track_set_batch(2)
+            want = [ref.track_frame(f) for f in frames]
+        for k in range(1, len(frames)):
+            T64, _, sto, _ = oracle.align(frames[k], frames[k - 1])
+            assert want[k][1] == sto and _pose_err(want[k][0], T64) <= POSE_TOL
+        with youth_icp.IcpContext(640, 480, max_frames) as ctx:
+            if batch_mode:
+                ctx.track_set_batch(2)
+            got = []
+            ctx.track_submit_batch(frames[0:2])            # no reference: prep + one align
+            got += [ctx.track_collect() for _ in range(2)]
+            ctx.track_submit_batch(frames[2:4])            # one chained launch
+            ctx.track_submit(frames[4])                    # a single behind it
+            got += [ctx.track_collect() for _ in range(3)]
+            for k in range(5, 11, 2):
+                ctx.track_submit_batch(frames[k:k + 2])
+                got.append(ctx.track_collect())
+                got.append(ctx.track_collect())
+            ctx.track_submit_batch(frames[11:12])          # a batch of one
+            got.append(ctx.track_collect())
+            chained = ctx.track_chained()
+            assert chained == (4 if batch_mode and max_frames >= 4 else 0), chained
+            assert ctx.track_pending() == 0 and len(got) == len(want)
+            for k, ((Tg, sg, hg), (Tw, sw, hw)) in enumerate(zip(got, want)):
+                assert np.array_equal(Tg, Tw) and sg == sw and hg == hw, (batch_mode, k)
+            with pytest.raises(youth_icp.IcpError):
+                ctx.track_submit_batch(frames[0:3])        # more than TRACK_MAX_BATCH
+            ctx.track_reset()
+            ctx.track_submit_batch(frames[0:2])
+            ctx.track_reset()                              # batch in flight
+            ctx.track_submit(frames[3])
+            hs = [ctx.track_collect()[2] for _ in range(3)]
+            assert hs == [False, True, False]
+            ctx.track_reset()
+            Tb, stb = ctx.track_host_sequence(frames)
+            assert np.array_equal(Tb, np.stack([w[0] for w in want[1:]]))
+            assert np.array_equal(stb, np.array([w[1] for w in want[1:]], np.int32))

@@ -8,7 +8,7 @@
 # Usage: tools/profile.sh <tag> [bench args...]
 set -euo pipefail
 TAG=${1:-r02}; shift || true
-ARGS=${*:---steps 30 --warmup 5 --windows 0 --no-cpu-baseline --no-host-io --no-legs --no-viewer}
+ARGS=${*:---steps 30 --warmup 5 --windows 0 --no-cpu-baseline --no-host-io --no-legs --no-viewer --no-spec-parity}
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/prof_$TAG
 mkdir -p $OUT
