@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
-"""Tracker micro-batch probe (run under rocprofv3 --kernel-trace): the same
-host sequence through (a) the default plan, one launch per frame; (b) the
-batch plan (youth_icp_track_set_batch(2)) one launch per frame; (c) the batch
-plan in micro-batches of two frames.  Prints frames/s of each."""
+"""Tracker micro-batch probe (run alone or under rocprofv3 --kernel-trace):
+the same host sequence through (a) the default plan, one launch per frame;
+(b) the batch plan (youth_icp_track_set_batch(2)) one launch per frame;
+(c) the batch plan in micro-batches of two frames through the library's C
+loop; (d) the same micro-batches from a Python loop with the host time of
+each submit and collect.  Prints frames/s of each."""
 import os
 import sys
 import time
@@ -36,6 +38,28 @@ def run(ctx, batch_submit):
     return n / (time.perf_counter() - t0)
 
 
+def run_py_batches(ctx, in_flight):
+    """micro-batches from Python; returns (frames/s, median submit us,
+    median collect-wait us)"""
+    ctx.track_reset()
+    ts, tc = [], []
+    t0 = time.perf_counter()
+    ctx.track_submit(frames[0])
+    for f in range(1, n, 2):
+        m = min(2, n - f)
+        while ctx.track_pending() + m > in_flight:
+            a = time.perf_counter()
+            ctx.track_collect()
+            tc.append(time.perf_counter() - a)
+        a = time.perf_counter()
+        ctx.track_submit_batch(frames[f:f + m])
+        ts.append(time.perf_counter() - a)
+    while ctx.track_pending():
+        ctx.track_collect()
+    rate = n / (time.perf_counter() - t0)
+    return rate, 1e6 * float(np.median(ts)), 1e6 * float(np.median(tc))
+
+
 a = youth_icp.IcpContext(640, 480, 4)
 run(a, False)
 print("default plan, per frame:", round(run(a, False)), a.get_plan(), flush=True)
@@ -44,5 +68,10 @@ b.track_set_batch(2)
 run(b, False)
 print("batch plan, per frame:", round(run(b, False)), b.get_plan(), flush=True)
 run(b, True)
-print("batch plan, micro-batches:", round(run(b, True)), b.get_plan(), "chained", b.track_chained(),
-      flush=True)
+print("batch plan, micro-batches (C loop):", round(run(b, True)), b.get_plan(), "chained",
+      b.track_chained(), flush=True)
+for inf in (2, 4):
+    run_py_batches(b, inf)
+    r, s, c = run_py_batches(b, inf)
+    print(f"batch plan, micro-batches (Python, {inf} in flight): {round(r)} frames/s, "
+          f"submit {s:.1f} us, collect wait {c:.1f} us (medians)", flush=True)
