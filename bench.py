@@ -721,8 +721,9 @@ def streamed_rate(a, frames, rel_batch, passes=5):
         Tb, _ = ctx2.track_host_sequence(frames)
         r_b.append(n / (time.perf_counter() - t0))
     chained = ctx2.track_chained()
-    # the same mode frame by frame (batch mode's 256-thread plan): the
-    # batched poses must equal it bit for bit
+    # the same mode frame by frame (batch mode's plan: the fewest source
+    # pixels per lane whose two grids fit the chip, 5 at 640x480): the batched
+    # poses must equal it bit for bit
     ctx2.track_reset()
     sync_b = [T for T, _, has in (ctx2.track_frame(f) for f in frames) if has]
     ctx2.close()
@@ -741,7 +742,7 @@ def streamed_rate(a, frames, rel_batch, passes=5):
             "batched_equals_sync": bool(np.array_equal(Tb, np.stack(sync_b))),
             "batched_launches": chained,
             "batched_max_abs_diff_vs_per_frame_plan": pose_err(Tb, np.stack(sync)),
-            "in_flight": 2,
+            "in_flight": 2, "batched_in_flight": 2 * youth_icp.TRACK_MAX_BATCH,
             "note": "host frames, copy to pinned + H2D + align + pose to pinned per frame; value: "
                     "the faster of youth_icp_track_host_sequence with one launch per frame (two "
                     "in flight: per_frame_value) and with micro-batches of two frames "

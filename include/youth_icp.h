@@ -420,6 +420,9 @@ int youth_slam_get_pose(int index, uint32_t* timestamp, double* T_wc);
 /* Block until the ingest queue is empty and the worker is idle, or
  * timeout_ms elapses.  Returns 1 when drained, 0 on timeout / not running. */
 int youth_slam_wait_idle(int timeout_ms);
+/* Frames the worker has tracked in micro-batches of two since the module
+ * started (YOUTH_SLAM_TRACK_BATCH=2 with a backlogged queue; 0 otherwise). */
+long long youth_slam_batched_frames(void);
 /* Block until the module stops (used by algorithmModule). */
 void youth_slam_wait_stopped(void);
 

@@ -159,6 +159,7 @@ std::atomic<bool> g_running{false};
 std::atomic<bool> g_process{false};  // SLAM.cpp:29 process_frames
 std::atomic<bool> g_busy{false};
 std::atomic<bool> g_reset{false};
+std::atomic<long long> g_batched{0};  // frames tracked in micro-batches
 std::thread g_worker;
 youth_frame_queue* g_queue = nullptr;
 
@@ -199,12 +200,23 @@ youth_intrinsics intrinsics_for(int w, int h)
 // while the host records k-1's pose and pops k+1.  A frame's pose reaches
 // the trajectory when the next frame is submitted or the queue runs empty
 // (the worker stays busy until then: youth_slam_wait_idle).
+// YOUTH_SLAM_TRACK_BATCH=2 (opt-in, for backlogged queues such as a .bin
+// replay): when a second frame of the same size is already queued, the two
+// are tracked as one micro-batch (youth_icp_track_submit_batch), two
+// submissions in flight; every frame then runs on the batch plan, so a pose
+// does not depend on whether its frame was batched.
 void worker_main(int device)
 {
     fprintf(stderr, "youth_icp: SLAM processing thread started\n");
     youth_icp_ctx* ctx = nullptr;
     int cw = 0, ch = 0;
+    const char* eb = getenv("YOUTH_SLAM_TRACK_BATCH");
+    const int batch = eb && atoi(eb) >= 2 ? 2 : 1;
+    const size_t kMaxFrame = (size_t)4096 * 4096;
     std::vector<int16_t> buf;
+    bool held = false;  // a popped frame not yet submitted, at buf[kMaxFrame]
+    int held_w = 0, held_h = 0;
+    uint32_t held_ts = 0;
     double T_w_ref[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
     struct Pending {
         uint32_t ts;
@@ -245,11 +257,20 @@ void worker_main(int device)
         g_last_points = pr0.npts;
     };
     while (g_process.load()) {
-        if (buf.empty()) buf.resize((size_t)4096 * 4096);
+        if (buf.empty()) buf.resize(kMaxFrame * batch);
         int w = 0, h = 0;
         uint32_t ts = 0;
         g_busy.store(true);
-        const int got = youth_queue_pop(g_queue, buf.data(), buf.size(), &w, &h, &ts);
+        int got = 1;
+        if (held) {
+            memmove(buf.data(), buf.data() + kMaxFrame, (size_t)held_w * held_h * sizeof(int16_t));
+            w = held_w;
+            h = held_h;
+            ts = held_ts;
+            held = false;
+        } else {
+            got = youth_queue_pop(g_queue, buf.data(), kMaxFrame, &w, &h, &ts);
+        }
         if (got != 1) {
             if (!pend.empty()) {  // nothing new: finish what is in flight
                 finish_one(true);
@@ -267,7 +288,7 @@ void worker_main(int device)
             while (!pend.empty()) finish_one(true);
             if (ctx) youth_icp_destroy(ctx);
             const youth_intrinsics K = intrinsics_for(w, h);
-            ctx = youth_icp_create(device, w, h, 2, &K, nullptr);
+            ctx = youth_icp_create(device, w, h, 2 * batch, &K, nullptr);
             cw = w;
             ch = h;
             if (!ctx) {
@@ -277,15 +298,51 @@ void worker_main(int device)
                 g_busy.store(false);
                 continue;
             }
+            if (batch > 1) youth_icp_track_set_batch(ctx, batch);
         }
-        int npts = 0;
-        for (size_t i = 0; i < (size_t)w * h; ++i) npts += buf[i] > 0;
-        if (youth_icp_track_submit(ctx, buf.data(), nullptr) < 0) {
+        const size_t N = (size_t)w * h;
+        auto count_points = [&](const int16_t* d) {
+            int n = 0;
+            for (size_t i = 0; i < N; ++i) n += d[i] > 0;
+            return n;
+        };
+        // micro-batch: a second frame of this size already waiting (one of
+        // another size, or of a sequence reset since, is held for the next
+        // round)
+        int m = 1;
+        uint32_t ts2 = 0;
+        if (batch > 1 && youth_queue_size(g_queue) > 0) {
+            int w2 = 0, h2 = 0;
+            if (youth_queue_pop(g_queue, buf.data() + kMaxFrame, kMaxFrame, &w2, &h2, &ts2) == 1) {
+                if (w2 == w && h2 == h && !g_reset.load()) {
+                    m = 2;
+                    memmove(buf.data() + N, buf.data() + kMaxFrame, N * sizeof(int16_t));
+                } else {
+                    held = true;
+                    held_w = w2;
+                    held_h = h2;
+                    held_ts = ts2;
+                }
+            }
+        }
+        // two submissions in flight: frames, or micro-batches of two
+        while (!pend.empty() && (int)pend.size() + m > 2 * batch) finish_one(true);
+        const long long chained0 = youth_icp_track_chained(ctx);
+        const int rc = m == 1 ? youth_icp_track_submit(ctx, buf.data(), nullptr)
+                              : youth_icp_track_submit_batch(ctx, buf.data(), m);
+        // frames that ran as one launch (a sequence's first frame is prepped alone)
+        g_batched.fetch_add(2 * (youth_icp_track_chained(ctx) - chained0));
+        if (rc < 0) {
             fprintf(stderr, "youth_icp: tracking failed: %s\n", youth_icp_last_error());
+            // a micro-batch may have submitted its first frame before failing
+            const int sent = youth_icp_track_pending(ctx) - (int)pend.size();
+            for (int i = 0; i < sent && i < m; ++i)
+                pend.push_back(Pending{i ? ts2 : ts, count_points(buf.data() + i * N)});
             continue;
         }
-        pend.push_back(Pending{ts, npts});
-        if (pend.size() == 2) finish_one(true);
+        pend.push_back(Pending{ts, count_points(buf.data())});
+        if (m == 2) pend.push_back(Pending{ts2, count_points(buf.data() + N)});
+        if (batch == 1 && pend.size() == 2) finish_one(true);
     }
     while (ctx && !pend.empty()) finish_one(true);
     if (ctx) youth_icp_destroy(ctx);
@@ -388,6 +445,7 @@ void initSlamModule(const char* config_file, const char* vocabulary_file)
     g_traj.clear();
     g_last_points = 0;
     g_process.store(true);
+    g_batched.store(0);
     try {
         g_worker = std::thread(worker_main, device);
     } catch (const std::exception& ex) {
@@ -511,6 +569,8 @@ int youth_slam_get_pose(int index, uint32_t* timestamp, double* T_wc)
     if (T_wc) memcpy(T_wc, g_traj[index].T, sizeof(g_traj[index].T));
     return 1;
 }
+
+long long youth_slam_batched_frames(void) { return g_batched.load(); }
 
 int youth_slam_wait_idle(int timeout_ms)
 {

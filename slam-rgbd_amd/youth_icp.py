@@ -143,6 +143,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "youth_slam_trajectory_length": (c_int, []),
         "youth_slam_get_trajectory": (c_int, [c_int, POINTER(c_uint32), PD]),
         "youth_slam_wait_idle": (c_int, [c_int]),
+        "youth_slam_batched_frames": (ctypes.c_longlong, []),
         "youth_slam_wait_stopped": (None, []),
     }
     ab_build = bool(os.environ.get("YOUTH_ICP_LIB"))  # tools/ab_*.sh: older builds
@@ -240,6 +241,11 @@ def resetSlam() -> None:
 
 def slam_wait_idle(timeout_ms: int = 10000) -> int:
     return load_library().youth_slam_wait_idle(timeout_ms)
+
+
+def slam_batched_frames() -> int:
+    """Frames the SLAM worker tracked in micro-batches (YOUTH_SLAM_TRACK_BATCH=2)."""
+    return int(load_library().youth_slam_batched_frames())
 
 
 def slam_trajectory() -> tuple[np.ndarray, np.ndarray]:

@@ -503,6 +503,39 @@ def test_slam_api_end_to_end():
     assert youth_icp.processSlamFrame(frames[0], None, 640, 480, 0) == 0
 
 
+def test_slam_worker_micro_batches(monkeypatch):
+    """YOUTH_SLAM_TRACK_BATCH=2: a backlogged queue (9 frames pushed at once,
+    under the reference's drop threshold of 10) is tracked in micro-batches
+    of two.  Every pose is the one the batch plan gives frame by frame
+    (composition aside: world poses within 1e-12 of the prefix product of
+    the context's relative poses) and within 1e-5 of the oracle's."""
+    monkeypatch.setenv("YOUTH_SLAM_TRACK_BATCH", "2")
+    F = 9
+    frames, _ = youth_synth.sequence(0, F)
+    youth_icp.initSlamModule(os.path.join(GOLDEN, "astra_camera.yaml"), "ORBvoc.txt")
+    try:
+        for k in range(F):
+            assert youth_icp.processSlamFrame(frames[k], None, 640, 480, 100 + k) == 1
+        assert youth_icp.slam_wait_idle(20000) == 1
+        ts, T = youth_icp.slam_trajectory()
+        batched = youth_icp.slam_batched_frames()
+    finally:
+        youth_icp.stopSlamModule()
+    assert list(ts) == [100 + k for k in range(F)]
+    assert batched >= 2, batched
+    K = youth_icp.parse_camera_yaml(os.path.join(GOLDEN, "astra_camera.yaml"))[0]
+    with youth_icp.IcpContext(640, 480, 4, K=K) as ctx:
+        ctx.track_set_batch(2)
+        rel = [ctx.track_frame(f)[0] for f in frames][1:]
+    acc, acc_o = np.eye(4), np.eye(4)
+    assert np.array_equal(T[0], acc)
+    for k in range(1, F):
+        acc = acc @ rel[k - 1]
+        acc_o = acc_o @ oracle.align(frames[k], frames[k - 1])[0]
+        assert _pose_err(T[k], acc) <= 1e-12
+        assert _pose_err(T[k], acc_o) <= POSE_TOL
+
+
 def test_algorithm_module_thread_entry(monkeypatch):
     import threading
     import youth_wire

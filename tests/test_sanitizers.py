@@ -2,7 +2,7 @@
 item 9): tests/tsan/driver.cpp drives the SLAM.h queue + worker
 (slam_api.cpp), the AlgorithmModule frame loop and its POSIX-queue transport
 (wire.c, algorithm_module.c) from many threads at once, built with
--fsanitize=thread and with -fsanitize=address,undefined.  The six device
+-fsanitize=thread and with -fsanitize=address,undefined.  The device
 entry points the worker calls come from tests/tsan/icp_stub.c (a CPU
 stand-in linked only into this driver), so it runs without a GPU.  Host code
 only: GPU sanitizers are not available on the GPU pool.
@@ -24,11 +24,16 @@ def drivers():
     return TSAN
 
 
+TSAN_ENV = {"TSAN_OPTIONS": "halt_on_error=1 second_deadlock_stack=1"}
+ASAN_ENV = {"ASAN_OPTIONS": "detect_leaks=1 abort_on_error=0",
+            "UBSAN_OPTIONS": "halt_on_error=1 print_stacktrace=1"}
+BATCH = {"YOUTH_SLAM_TRACK_BATCH": "2"}     # the worker's micro-batch mode
+
+
 @pytest.mark.parametrize("kind,env", [
-    ("tsan", {"TSAN_OPTIONS": "halt_on_error=1 second_deadlock_stack=1"}),
-    ("asan", {"ASAN_OPTIONS": "detect_leaks=1 abort_on_error=0",
-              "UBSAN_OPTIONS": "halt_on_error=1 print_stacktrace=1"}),
-])
+    ("tsan", TSAN_ENV), ("asan", ASAN_ENV),
+    ("tsan", {**TSAN_ENV, **BATCH}), ("asan", {**ASAN_ENV, **BATCH}),
+], ids=["tsan", "asan", "tsan-batch", "asan-batch"])
 def test_host_threading_under_sanitizer(drivers, kind, env):
     r = subprocess.run([os.path.join(drivers, "driver_" + kind)], capture_output=True, text=True,
                        timeout=300, env={**os.environ, **env})

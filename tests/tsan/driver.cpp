@@ -81,6 +81,8 @@ static void scenario_init_and_producers()
     });
     for (auto& p : prod) p.join();
     check(youth_slam_wait_idle(20000) == 1, "worker idle");
+    if (getenv("YOUTH_SLAM_TRACK_BATCH"))
+        check(youth_slam_batched_frames() > 0, "worker tracked micro-batches");
     done.store(true);
     reader.join();
     const int len = youth_slam_trajectory_length();

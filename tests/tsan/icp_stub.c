@@ -2,7 +2,8 @@
  * icp_stub.c — TEST INFRASTRUCTURE ONLY: a CPU stand-in for the
  * libyouth_icp device entry points the host-side threading code calls
  * (slam_api.cpp's worker: create / destroy / track_submit / track_collect /
- * track_frame / track_reset / device_count / last_error, plus
+ * track_frame / track_reset / track_submit_batch / track_set_batch /
+ * track_chained / device_count / last_error, plus
  * youth_default_intrinsics), so the SLAM.h
  * queue + worker, the AlgorithmModule frame loop and the POSIX-queue
  * transport can run under ThreadSanitizer / AddressSanitizer on a machine
@@ -23,7 +24,8 @@ struct youth_icp_ctx {
     long long ref_sum;
     /* submitted frames' results, oldest first */
     double T[YOUTH_TRACK_MAX_IN_FLIGHT][16];
-    int has[YOUTH_TRACK_MAX_IN_FLIGHT], n, head;
+    int has[YOUTH_TRACK_MAX_IN_FLIGHT], n, head, batch;
+    long long chained;
 };
 
 int youth_icp_device_count(void) { return 1; }
@@ -72,6 +74,28 @@ int youth_icp_track_collect(youth_icp_ctx* c, double* T_rel, int* has_ref)
 }
 
 int youth_icp_track_pending(const youth_icp_ctx* c) { return c->n; }
+
+int youth_icp_track_set_batch(youth_icp_ctx* c, int frames)
+{
+    const int old = c->batch ? c->batch : 1;
+    c->batch = frames;
+    return old;
+}
+
+long long youth_icp_track_chained(const youth_icp_ctx* c) { return c->chained; }
+
+/* as the library: a sequence's first frame alone, then one "launch" */
+int youth_icp_track_submit_batch(youth_icp_ctx* c, const int16_t* depth, int n_frames)
+{
+    if (n_frames < 1 || n_frames > YOUTH_TRACK_MAX_BATCH ||
+        c->n + n_frames > YOUTH_TRACK_MAX_IN_FLIGHT)
+        return YOUTH_EINVAL;
+    const int chain = c->has_ref && n_frames > 1;
+    for (int i = 0; i < n_frames; ++i)
+        youth_icp_track_submit(c, depth + (size_t)i * c->W * c->H, NULL);
+    c->chained += chain;
+    return 0;
+}
 
 int youth_icp_track_frame(youth_icp_ctx* c, const int16_t* depth, const double* T_init,
                           double* T_rel, int* has_ref)

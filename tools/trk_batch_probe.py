@@ -68,8 +68,9 @@ b.track_set_batch(2)
 run(b, False)
 print("batch plan, per frame:", round(run(b, False)), b.get_plan(), flush=True)
 run(b, True)
-print("batch plan, micro-batches (C loop):", round(run(b, True)), b.get_plan(), "chained",
-      b.track_chained(), flush=True)
+print("batch plan, micro-batches (C loop):", [round(run(b, True)) for _ in range(5)], b.get_plan(),
+      "chained", b.track_chained(), flush=True)
+print("default plan, per frame (C loop):", [round(run(a, True)) for _ in range(5)], flush=True)
 for inf in (2, 4):
     run_py_batches(b, inf)
     r, s, c = run_py_batches(b, inf)
