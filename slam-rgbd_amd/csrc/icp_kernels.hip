@@ -1097,60 +1097,88 @@ struct PoseState {
 //   kSpecSurvey: P'_i = ((R_i0 x + R_i1 y) + R_i2 z) + t_i and
 //       u' = floor(((fx P'_x) / P'_z + cx) + 0.5), the
 //       quotient IEEE (proj_quot on the shared correctly rounded reciprocal).
+// Lane masks (one bit per lane of the wave, bit set only on active lanes):
+// compares go straight to SGPR masks (v_cmp), combine on the scalar unit and
+// feed selects through inverse_ballot, and a wave's match count is one
+// s_bcnt1; a per-lane boolean would be rebuilt from a 0/1 select and a
+// compare wherever it is counted (two 4-cycle VALU forms per pixel).
+typedef unsigned long long LaneMask;
+constexpr int kFcmpOgt = 2, kFcmpOlt = 4, kIcmpUlt = 36, kIcmpUle = 37;
+__device__ __forceinline__ LaneMask mask_gt(float a, float b) { return __builtin_amdgcn_fcmpf(a, b, kFcmpOgt); }
+__device__ __forceinline__ LaneMask mask_lt(float a, float b) { return __builtin_amdgcn_fcmpf(a, b, kFcmpOlt); }
+__device__ __forceinline__ LaneMask mask_ult(unsigned a, unsigned b) { return __builtin_amdgcn_uicmp(a, b, kIcmpUlt); }
+__device__ __forceinline__ LaneMask mask_ule(unsigned a, unsigned b) { return __builtin_amdgcn_uicmp(a, b, kIcmpUle); }
+__device__ __forceinline__ bool lane_in(LaneMask m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+
 template <int kSp>
 __device__ __forceinline__ void xform_project(const float* T, float sx, float sy, float sz,
                                               const Intr& K, int W, int H, float& qx, float& qy,
-                                              float& qz, float& fu, float& fv, bool& in, int& j)
+                                              float& qz, float& fu, float& fv, LaneMask& inm, int& j)
 {
-    float uu, vv;
-    bool vz;
     if (kSp == kSpecSurvey) {
         qx = ((T[0] * sx + T[1] * sy) + T[2] * sz) + T[3];
         qy = ((T[4] * sx + T[5] * sy) + T[6] * sz) + T[7];
         qz = ((T[8] * sx + T[9] * sy) + T[10] * sz) + T[11];
-        vz = (sz > 0.0f) & (qz > 0.0f);
-        const float den = vz ? qz : 1.0f;
         const float nu = K.fx * qx, nv = K.fy * qy;
-        float pu, pv;
-        if (proj_den_ok(den)) {  // always in practice (den is a depth in metres)
-            const float r = proj_recip(den);
-            pu = proj_quot(nu, den, r);
-            pv = proj_quot(nv, den, r);
-        } else {
-            pu = nu / den;
-            pv = nv / den;
+        // P'_z in [2^-60, 2^60] (proj_den_ok, which implies P'_z > 0) as ONE
+        // unsigned compare on its bits (negative and NaN bit patterns lie
+        // above 2^60's): every lane takes the fast quotient with den = P'_z;
+        // a valid source whose P'_z is <= 0 or outside the range (never in
+        // practice) redoes it below as the IEEE division of the spec.  The
+        // other lanes' quotients may be inf / NaN; the mask drops them.
+        const LaneMask sok = mask_gt(sz, 0.0f);
+        const LaneMask dok = mask_ule(__float_as_uint(qz) - 0x21800000u, 0x5d800000u - 0x21800000u);
+        const float r = proj_recip(qz);
+        float pu = proj_quot(nu, qz, r);
+        float pv = proj_quot(nv, qz, r);
+        LaneMask vz = sok & dok;
+        const LaneMask slow = sok & ~dok;
+        if (__builtin_expect(slow != 0, 0)) {  // wave-uniform
+            const LaneMask qpos = mask_gt(qz, 0.0f);
+            if (lane_in(slow)) {
+                const float den = lane_in(qpos) ? qz : 1.0f;
+                pu = nu / den;
+                pv = nv / den;
+            }
+            vz |= slow & qpos;
         }
         // floor, in-range test and the pixel index without selects: the
         // coordinates stay finite on every lane (saturated integers), and an
         // unmatched lane's gather is masked after it (a raw buffer load past
-        // the records returns 0, any index inside them is a real record)
+        // the records returns 0, any index inside them is a real record).
+        // The row test is the records' own: v' outside [0, H) is clamped to
+        // H, whose index lies in the frame's zeroed pad (P >= N + 4) or past
+        // the buffer (returns 0), a record with z = 0, which the match gate
+        // (tz > 0) rejects as it rejects a target without a normal
         const int iu = floor_i32((pu + K.cx) + 0.5f);
         const int iv = floor_i32((pv + K.cy) + 0.5f);
-        in = vz & ((unsigned)iu < (unsigned)W) & ((unsigned)iv < (unsigned)H);
+        const unsigned ivc = min((unsigned)iv, (unsigned)H);
+        inm = vz & mask_ult((unsigned)iu, (unsigned)W);
         fu = (float)iu;
         fv = (float)iv;
-        j = (int)(__umul24((unsigned)iv, (unsigned)W) + (unsigned)iu);
-        return;
+        j = (int)(__umul24(ivc, (unsigned)W) + (unsigned)iu);
     } else {
         qx = fmaf(T[2], sz, fmaf(T[1], sy, fmaf(T[0], sx, T[3])));
         qy = fmaf(T[6], sz, fmaf(T[5], sy, fmaf(T[4], sx, T[7])));
         qz = fmaf(T[10], sz, fmaf(T[9], sy, fmaf(T[8], sx, T[11])));
-        vz = (sz > 0.0f) & (qz > 0.0f);
-        const float rz = proj_rcp_rn(vz ? qz : 1.0f);
-        uu = floorf(fmaf(K.fx * qx, rz, K.cx + 0.5f));
-        vv = floorf(fmaf(K.fy * qy, rz, K.cy + 0.5f));
+        const LaneMask vz = mask_gt(sz, 0.0f) & mask_gt(qz, 0.0f);
+        const float rz = proj_rcp_rn(lane_in(vz) ? qz : 1.0f);
+        const float uu = floorf(fmaf(K.fx * qx, rz, K.cx + 0.5f));
+        const float vv = floorf(fmaf(K.fy * qy, rz, K.cy + 0.5f));
+        // 0 <= u' < W and 0 <= v' < H on the integer values: uu, vv are
+        // finite integral floats (T finite, youth_icp.h), v_cvt_i32_f32
+        // saturates outside the int range, and a negative one wraps to
+        // >= 2^31 unsigned, so the unsigned compares equal the spec's four
+        // float compares
+        const int iu = (int)uu, iv = (int)vv;
+        inm = vz & mask_ult((unsigned)iu, (unsigned)W) & mask_ult((unsigned)iv, (unsigned)H);
+        const bool in = lane_in(inm);
+        fu = in ? uu : 0.0f;
+        fv = in ? vv : 0.0f;
+        // 0 when !in; v', W <= 16384 (youth_icp_create): the 24-bit
+        // multiply-add is exact and full rate
+        j = in ? (int)__umul24((unsigned)iv, (unsigned)W) + iu : 0;
     }
-    // 0 <= u' < W and 0 <= v' < H on the integer values: uu, vv are finite
-    // integral floats (T finite, youth_icp.h), v_cvt_i32_f32 saturates
-    // outside the int range, and a negative one wraps to >= 2^31 unsigned,
-    // so the unsigned compares equal the spec's four float compares
-    const int iu = (int)uu, iv = (int)vv;
-    in = vz & ((unsigned)iu < (unsigned)W) & ((unsigned)iv < (unsigned)H);
-    fu = in ? uu : 0.0f;
-    fv = in ? vv : 0.0f;
-    // 0 when !in; v', W <= 16384 (youth_icp_create): the 24-bit multiply-add
-    // is exact and full rate
-    j = in ? (int)__umul24((unsigned)iv, (unsigned)W) + iu : 0;
 }
 
 //   a7  gate: target valid with a normal (k_prep stores z = 0 for a target
@@ -1165,9 +1193,9 @@ __device__ __forceinline__ void xform_project(const float* T, float sx, float sy
 //   kSpecSurvey: d2 = (dx dx + dy dy) + dz dz, r = (n0 dx + n1 dy) + n2 dz,
 //       (P' x n)_0 = qy n2 - qz n1 etc. (no FMA).
 template <int kSp, bool kFast>
-__device__ __forceinline__ bool match_accumulate(float qx, float qy, float qz, f4v t, float fu,
-                                                 float fv, bool in, const Intr& K,
-                                                 const FastK& F, float thr2, double* acc)
+__device__ __forceinline__ LaneMask match_accumulate(float qx, float qy, float qz, f4v t, float fu,
+                                                     float fv, LaneMask inm, const Intr& K,
+                                                     const FastK& F, float thr2, double* acc)
 {
     const float tz = t.x;
     const float tx = bp_div<kFast>((fu - K.cx) * tz, K.fx, F.hfx, F.lfx);
@@ -1175,7 +1203,8 @@ __device__ __forceinline__ bool match_accumulate(float qx, float qy, float qz, f
     const float dx = qx - tx, dy = qy - ty, dz = qz - tz;
     const float d2 = kSp == kSpecSurvey ? (dx * dx + dy * dy) + dz * dz
                                         : fmaf(dz, dz, fmaf(dy, dy, dx * dx));
-    const bool ok = in & (tz > 0.0f) & (d2 < thr2);
+    const LaneMask okm = inm & mask_gt(tz, 0.0f) & mask_lt(d2, thr2);
+    const bool ok = lane_in(okm);
     const float n0 = ok ? t.y : 0.0f, n1 = ok ? t.z : 0.0f, n2 = ok ? t.w : 0.0f;
     float r, Jf[6];
     if (kSp == kSpecSurvey) {
@@ -1203,7 +1232,7 @@ __device__ __forceinline__ bool match_accumulate(float qx, float qy, float qz, f
 #pragma unroll
     for (int a = 0; a < 6; ++a) acc[21 + a] = fma((double)Jf[a], (double)r, acc[21 + a]);
     acc[27] = fma((double)r, (double)r, acc[27]);
-    return ok;
+    return okm;
 }
 
 // Accumulate source pixels [start, end) of one pair into acc (spec a7-a9).
@@ -1235,7 +1264,7 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
         const short4 d4 = load_depth4<kAligned>(sD, i, end);
         const int dd[4] = {d4.x, d4.y, d4.z, d4.w};
         float qx[4], qy[4], qz[4], fu[4], fv[4];
-        bool in[4];
+        LaneMask in[4];
         int j[4];
         // a lane's four pixels share one row when kAligned: centred
         // coordinates by exact additions (uc0 + q == (float)(u0 + q) - cx)
@@ -1269,13 +1298,16 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
                                                                                  0, 0));
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const bool ok = match_accumulate<kSp, kFast>(qx[q], qy[q], qz[q], t[q], fu[q], fv[q],
-                                                         in[q], K, F, thr2, acc);
-            if (kAssoc && (i + q) < end) arow[i + q] = ok ? j[q] : -1;
-            cnt += ok ? 1 : 0;
+            const LaneMask okm = match_accumulate<kSp, kFast>(qx[q], qy[q], qz[q], t[q], fu[q],
+                                                              fv[q], in[q], K, F, thr2, acc);
+            if (kAssoc && (i + q) < end) arow[i + q] = lane_in(okm) ? j[q] : -1;
+            // matches counted per wave on the scalar unit (s_bcnt1 of the
+            // match mask) instead of a per-lane select and add
+            cnt += __builtin_popcountll(okm);
         }
     }
-    acc[28] += (double)cnt;
+    // the wave's count, carried by lane 0 into the wave / workgroup sums
+    acc[28] += (threadIdx.x & 63) == 0 ? (double)cnt : 0.0;
 }
 
 // Wave sum of the kNeq per-lane accumulators by recursive halving: at lane
@@ -1882,7 +1914,7 @@ __device__ __forceinline__ void coop_group(const float* __restrict__ X, const fl
 {
     const int t = threadIdx.x;
     float qx[Q], qy[Q], qz[Q], fu[Q], fv[Q];
-    bool in[Q];
+    LaneMask in[Q];
     int j[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
@@ -1897,9 +1929,8 @@ __device__ __forceinline__ void coop_group(const float* __restrict__ X, const fl
         rec[q] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rrec, (int)((unsigned)j[q] * 16u), 0, 0));
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-        const bool ok = match_accumulate<kSp, kFast>(qx[q], qy[q], qz[q], rec[q], fu[q], fv[q],
-                                                     in[q], K, F, thr2, acc);
-        nmatch += ok ? 1 : 0;
+        nmatch += __builtin_popcountll(match_accumulate<kSp, kFast>(
+            qx[q], qy[q], qz[q], rec[q], fu[q], fv[q], in[q], K, F, thr2, acc));  // per wave
     }
 }
 
@@ -2072,7 +2103,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
         case 1: coop_group<kSp, kFast, 1, kThreads>(X, Y, Z, s0, T, rrec, W, H, K, F, thr2, acc, nmatch); break;
         default: break;
         }
-        acc[28] = (double)nmatch;
+        acc[28] = lane == 0 ? (double)nmatch : 0.0;  // the wave's count, lane 0
         COOP_MARK(k, 1);
         if (wave < 4) COOP_MARK_WAVE(k, 11 + wave);  // slots 12-14: waves 1-3 pixel loop done
         {
