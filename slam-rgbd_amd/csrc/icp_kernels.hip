@@ -1187,12 +1187,12 @@ __device__ __forceinline__ void xform_project(const float* T, float sx, float sy
 //   a8  r = n.(P' - P_t) = fma(n2, dz, fma(n1, dy, n0 dx));
 //       J = [P' x n, n], (P' x n)_0 = fma(qy, n2, -(qz n1)) etc.;
 //   a9  the 28 products of fp32 values are exact in fp64; one rounding per
-//       add.  Unmatched: the normal is masked to 0, so J = 0 and r = +-0 leave
-//       every sum unchanged.  The target's x, y are recomputed from its z with
+//       add.  Unmatched lanes skip the update, or add J = 0 and r = +-0,
+//       which leaves every sum unchanged.  The target's x, y are recomputed from its z with
 //       k_prep's expression (bit-identical to the stored plane).
 //   kSpecSurvey: d2 = (dx dx + dy dy) + dz dz, r = (n0 dx + n1 dy) + n2 dz,
 //       (P' x n)_0 = qy n2 - qz n1 etc. (no FMA).
-template <int kSp, bool kFast>
+template <int kSp, bool kFast, bool kSkip>
 __device__ __forceinline__ LaneMask match_accumulate(float qx, float qy, float qz, f4v t, float fu,
                                                      float fv, LaneMask inm, const Intr& K,
                                                      const FastK& F, float thr2, double* acc)
@@ -1204,34 +1204,44 @@ __device__ __forceinline__ LaneMask match_accumulate(float qx, float qy, float q
     const float d2 = kSp == kSpecSurvey ? (dx * dx + dy * dy) + dz * dz
                                         : fmaf(dz, dz, fmaf(dy, dy, dx * dx));
     const LaneMask okm = inm & mask_gt(tz, 0.0f) & mask_lt(d2, thr2);
+    // kSkip (the throughput kernels): unmatched lanes leave the sums
+    // unchanged by not running the update (exec-masked; a wave without a
+    // match skips it), k_icp 2 % faster than masking the normal.  Else
+    // (k_icp_coop, latency-bound: the branches cost it 5 %,
+    // profiles/r03/ab_exec_mask.txt) the normal is masked to 0, so J = 0 and
+    // r = +-0 add +0 exactly: the same sums either way
     const bool ok = lane_in(okm);
-    const float n0 = ok ? t.y : 0.0f, n1 = ok ? t.z : 0.0f, n2 = ok ? t.w : 0.0f;
-    float r, Jf[6];
-    if (kSp == kSpecSurvey) {
-        r = (n0 * dx + n1 * dy) + n2 * dz;
-        Jf[0] = qy * n2 - qz * n1;
-        Jf[1] = qz * n0 - qx * n2;
-        Jf[2] = qx * n1 - qy * n0;
-    } else {
-        r = fmaf(n2, dz, fmaf(n1, dy, n0 * dx));
-        Jf[0] = fmaf(qy, n2, -(qz * n1));
-        Jf[1] = fmaf(qz, n0, -(qx * n2));
-        Jf[2] = fmaf(qx, n1, -(qy * n0));
-    }
-    Jf[3] = n0;
-    Jf[4] = n1;
-    Jf[5] = n2;
-    int k = 0;
-#pragma unroll
-    for (int a = 0; a < 6; ++a)
-#pragma unroll
-        for (int bb = a; bb < 6; ++bb) {
-            acc[k] = fma((double)Jf[a], (double)Jf[bb], acc[k]);
-            ++k;
+    if (!kSkip || ok) {
+        const float n0 = kSkip || ok ? t.y : 0.0f;
+        const float n1 = kSkip || ok ? t.z : 0.0f;
+        const float n2 = kSkip || ok ? t.w : 0.0f;
+        float r, Jf[6];
+        if (kSp == kSpecSurvey) {
+            r = (n0 * dx + n1 * dy) + n2 * dz;
+            Jf[0] = qy * n2 - qz * n1;
+            Jf[1] = qz * n0 - qx * n2;
+            Jf[2] = qx * n1 - qy * n0;
+        } else {
+            r = fmaf(n2, dz, fmaf(n1, dy, n0 * dx));
+            Jf[0] = fmaf(qy, n2, -(qz * n1));
+            Jf[1] = fmaf(qz, n0, -(qx * n2));
+            Jf[2] = fmaf(qx, n1, -(qy * n0));
         }
+        Jf[3] = n0;
+        Jf[4] = n1;
+        Jf[5] = n2;
+        int k = 0;
 #pragma unroll
-    for (int a = 0; a < 6; ++a) acc[21 + a] = fma((double)Jf[a], (double)r, acc[21 + a]);
-    acc[27] = fma((double)r, (double)r, acc[27]);
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+            for (int bb = a; bb < 6; ++bb) {
+                acc[k] = fma((double)Jf[a], (double)Jf[bb], acc[k]);
+                ++k;
+            }
+#pragma unroll
+        for (int a = 0; a < 6; ++a) acc[21 + a] = fma((double)Jf[a], (double)r, acc[21 + a]);
+        acc[27] = fma((double)r, (double)r, acc[27]);
+    }
     return okm;
 }
 
@@ -1298,8 +1308,9 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
                                                                                  0, 0));
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const LaneMask okm = match_accumulate<kSp, kFast>(qx[q], qy[q], qz[q], t[q], fu[q],
-                                                              fv[q], in[q], K, F, thr2, acc);
+            const LaneMask okm = match_accumulate<kSp, kFast, true>(qx[q], qy[q], qz[q], t[q],
+                                                                    fu[q], fv[q], in[q], K, F,
+                                                                    thr2, acc);
             if (kAssoc && (i + q) < end) arow[i + q] = lane_in(okm) ? j[q] : -1;
             // matches counted per wave on the scalar unit (s_bcnt1 of the
             // match mask) instead of a per-lane select and add
@@ -1929,7 +1940,7 @@ __device__ __forceinline__ void coop_group(const float* __restrict__ X, const fl
         rec[q] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rrec, (int)((unsigned)j[q] * 16u), 0, 0));
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-        nmatch += __builtin_popcountll(match_accumulate<kSp, kFast>(
+        nmatch += __builtin_popcountll(match_accumulate<kSp, kFast, false>(
             qx[q], qy[q], qz[q], rec[q], fu[q], fv[q], in[q], K, F, thr2, acc));  // per wave
     }
 }
