@@ -138,19 +138,14 @@ __device__ __forceinline__ float bp_div(float n, float d, float h, float l)
 //     q = div_fmas(fma(-s,q,n), r, q); result = div_fixup(q, b, a)   (`make asm`).
 // For b in [2^-60, 2^60] div_scale rescales neither operand except when a is
 // 0, |a/b| >= ~2^95, |a/b| < 2^-126 or |a| < 2^-103; otherwise div_fmas is a
-// plain fma and div_fixup returns q unchanged, so the chain below equals a/b
-// bit for bit, and its reciprocal part depends on b only.  In the excepted
+// plain fma and div_fixup returns q unchanged, so q = RN(n r) with those two
+// fma corrections equals a/b bit for bit, and its reciprocal part depends on
+// b only (one correction suffices from a correctly rounded r: proj_quot).  In the excepted
 // cases the results differ at most between 0 / tiny / huge / inf / NaN
 // values, which the projection (+cx, +0.5, floor, range test) maps to the same
 // pixel or to "outside".  Callers fall back to a/b when b is out of range.
 // youth_icp_selftest_projdiv compares the two bitwise on random and edge
 // cases (tests/test_gpu_parity.py).
-__device__ __forceinline__ float proj_div_one(float n, float den, float r)
-{
-    float q = n * r;
-    q = fmaf(fmaf(-den, q, n), r, q);
-    return fmaf(fmaf(-den, q, n), r, q);
-}
 __device__ __forceinline__ float proj_recip(float den)
 {
     const float r0 = __builtin_amdgcn_rcpf(den);
@@ -221,7 +216,7 @@ __device__ __forceinline__ int floor_i32(float x)
 // x') > 0); unscale; return x for +-0 / +inf (`make asm`).  For x in
 // [2^-96, 2^118] the scaling and the class fix-up are identities, leaving
 // the sequence below.  The three quotients then share one reciprocal
-// (proj_div_one): len = sqrt(x) is in [2^-48, 2^59] and |c_i| <= ~len, so
+// (norm_div): len = sqrt(x) is in [2^-48, 2^59] and |c_i| <= ~len, so
 // div_scale rescales no operand when |c_i| >= 2^-64; c_i = 0
 // is exact through the sign: RN(c/len) = copysign(RN(|c|/len), c).  Callers
 // take the IEEE expressions when norm_fast_ok is false.
@@ -243,9 +238,25 @@ __device__ __forceinline__ bool norm_fast_ok(float len2, float cx, float cy, flo
     return (len2 >= 0x1p-96f) && (len2 <= 0x1p118f) && norm_comp_ok(cx) && norm_comp_ok(cy) &&
            norm_comp_ok(cz);
 }
+// The three quotients take ONE correction from the correctly rounded
+// reciprocal r = RN(1 / len) (proj_recip; len in [2^-48, 2^59]), as the
+// projection's proj_quot (Markstein's theorem; youth_icp_selftest_normalize
+// compares with IEEE c / sqrtf(len2) bitwise).
 __device__ __forceinline__ float norm_div(float c, float len, float r)
 {
-    return copysignf(proj_div_one(fabsf(c), len, r), c);
+    return copysignf(proj_quot(fabsf(c), len, r), c);
+}
+// norm_fast_ok on the bits, for k_prep: len2 (>= +0 or NaN) in [2^-96,
+// 2^118] as one unsigned compare; a component c is "tiny" (0 < |c| < 2^-64)
+// iff t = 2 bits(c) - 2 (sign shifted out, wrapping: +-0 -> 2^32 - 2) is
+// below 2 bits(2^-64) - 2, so the three tests are one min3 and one compare.
+// The self-test checks it equals norm_fast_ok on every random vector.
+__device__ __forceinline__ bool norm_fast_ok_bits(float len2, float cx, float cy, float cz)
+{
+    constexpr unsigned kLo = 0x0F800000u, kHi = 0x7A800000u, kTiny = 2u * 0x1F800000u - 2u;
+    const unsigned tx = (__float_as_uint(cx) << 1) - 2u, ty = (__float_as_uint(cy) << 1) - 2u,
+                   tz = (__float_as_uint(cz) << 1) - 2u;
+    return (int)((__float_as_uint(len2) - kLo) <= (kHi - kLo)) & (int)(min(min(tx, ty), tz) >= kTiny);
 }
 
 // viewerModule.c:341-345 with explicit intrinsics (bit-identical to the
@@ -431,7 +442,8 @@ __global__ void k_selftest_projquot(unsigned long long n, unsigned long long see
 //   bad[0]: sqrt_rn_mid(x) != sqrtf(x) over EVERY fp32 x in [2^-96, 2^118];
 //   bad[1]: bitwise differences of (nx, ny, nz) vs c / sqrtf(len2) over `n`
 //           random vectors (components of mixed magnitude down to 2^-110,
-//           each +-0 with probability 1/8), wherever norm_fast_ok holds;
+//           each +-0 with probability 1/8), wherever norm_fast_ok holds,
+//           plus every vector where norm_fast_ok_bits differs from it;
 //   bad[2]: number of random vectors that took the fast path (coverage).
 __global__ void k_selftest_normalize(unsigned long long n, unsigned long long seed,
                                      unsigned long long* bad)
@@ -459,6 +471,7 @@ __global__ void k_selftest_normalize(unsigned long long n, unsigned long long se
                                          (unsigned)(r & 0x7FFFFF));
         }
         const float len2 = (c[0] * c[0] + c[1] * c[1]) + c[2] * c[2];
+        b1 += norm_fast_ok_bits(len2, c[0], c[1], c[2]) != norm_fast_ok(len2, c[0], c[1], c[2]);
         if (!(len2 > 0.0f) || !norm_fast_ok(len2, c[0], c[1], c[2])) continue;
         ++nf;
         const float len = sqrt_rn_mid(len2), r = proj_recip(len), ref = sqrtf(len2);
@@ -537,9 +550,12 @@ __device__ __forceinline__ void prep_tile(const int16_t* __restrict__ dep, float
 
     const __amdgpu_buffer_rsrc_t rrec =
         __builtin_amdgcn_make_buffer_rsrc(R, (short)0, (int)(P * sizeof(float4)), 0x00020000);
+    // the row of each step is wave-uniform (ty = wave index): its tests and
+    // offsets stay on the scalar unit
+    const int tyw = __builtin_amdgcn_readfirstlane(ty);
 #pragma unroll
     for (int k = 0; k < kTH / (kThreads / 64); ++k) {
-        const int row = ty + (kThreads / 64) * k;
+        const int row = tyw + (kThreads / 64) * k;
         const int gx = x0 + tx, gy = y0 + row;
         if (gx >= W || gy >= H) continue;
         const size_t i = (size_t)gy * W + gx;
@@ -551,45 +567,47 @@ __device__ __forceinline__ void prep_tile(const int16_t* __restrict__ dep, float
             X[P + i] = py;
             X[2 * P + i] = pz;
         }
-        float nx = 0.0f, ny = 0.0f, nz = 0.0f;
-        bool has_n = false;
-        const bool inner = gx > 0 && gy > 0 && gx < W - 1 && gy < H - 1;
-        if (inner) {
-            const float zl = sZ[o - 1], zr = sZ[o + 1];
-            const float zu = sZ[o - kLdsW], zd = sZ[o + kLdsW];
-            if (pz > 0.0f && zl > 0.0f && zr > 0.0f && zu > 0.0f && zd > 0.0f) {
-                const float ax = sX[o + 1] - sX[o - 1];
-                const float ay = sY[o + 1] - sY[o - 1];
-                const float az = zr - zl;
-                const float bx = sX[o + kLdsW] - sX[o - kLdsW];
-                const float by = sY[o + kLdsW] - sY[o - kLdsW];
-                const float bz = zd - zu;
-                const float cx = ay * bz - az * by;
-                const float cy = az * bx - ax * bz;
-                const float cz = ax * by - ay * bx;
-                const float len2 = (cx * cx + cy * cy) + cz * cz;
-                if (len2 > 0.0f) {
-                    if (norm_fast_ok(len2, cx, cy, cz)) {
-                        const float len = sqrt_rn_mid(len2);
-                        const float r = proj_recip(len);
-                        nx = norm_div(cx, len, r);
-                        ny = norm_div(cy, len, r);
-                        nz = norm_div(cz, len, r);
-                    } else {
-                        const float len = sqrtf(len2);  // correctly rounded (checked in .s)
-                        nx = cx / len;
-                        ny = cy / len;
-                        nz = cz / len;
-                    }
-                    has_n = true;
-                    if (((nx * px + ny * py) + nz * pz) > 0.0f) {
-                        nx = -nx;
-                        ny = -ny;
-                        nz = -nz;
-                    }
-                }
-            }
+        // branch-free: every lane forms the normal from its LDS neighbours
+        // (the halo exists for every pixel of the tile) and the record is
+        // selected at the end.  Every z is >= +0 (back-projection of
+        // max(d, 0), 0 outside the image), so the five z > 0 tests are one
+        // test of their minimum, taken on the bits (the same order for
+        // non-negative floats; +0 is bits 0)
+        const bool inner = (gx > 0) & (gy > 0) & (gx < W - 1) & (gy < H - 1);
+        const float zl = sZ[o - 1], zr = sZ[o + 1];
+        const float zu = sZ[o - kLdsW], zd = sZ[o + kLdsW];
+        const unsigned zmin = min(min(min(__float_as_uint(pz), __float_as_uint(zl)),
+                                      min(__float_as_uint(zr), __float_as_uint(zu))),
+                                  __float_as_uint(zd));
+        const float ax = sX[o + 1] - sX[o - 1];
+        const float ay = sY[o + 1] - sY[o - 1];
+        const float az = zr - zl;
+        const float bx = sX[o + kLdsW] - sX[o - kLdsW];
+        const float by = sY[o + kLdsW] - sY[o - kLdsW];
+        const float bz = zd - zu;
+        const float cx = ay * bz - az * by;
+        const float cy = az * bx - ax * bz;
+        const float cz = ax * by - ay * bx;
+        const float len2 = (cx * cx + cy * cy) + cz * cz;
+        const bool has_n = inner & (zmin != 0u) & (len2 > 0.0f);
+        const float len = sqrt_rn_mid(len2);
+        const float r = proj_recip(len);
+        float nx = norm_div(cx, len, r);
+        float ny = norm_div(cy, len, r);
+        float nz = norm_div(cz, len, r);
+        if (__builtin_expect(has_n & !norm_fast_ok_bits(len2, cx, cy, cz), 0)) {
+            const float l = sqrtf(len2);  // correctly rounded (checked in .s)
+            nx = cx / l;
+            ny = cy / l;
+            nz = cz / l;
         }
+        // oriented so n.P <= 0
+        if (((nx * px + ny * py) + nz * pz) > 0.0f) {
+            nx = -nx;
+            ny = -ny;
+            nz = -nz;
+        }
+        if (!has_n) nx = ny = nz = 0.0f;
         // a target without a normal is stored as z = 0 ("invalid target"):
         // the spec's two tests "target valid" and "normal valid" become the
         // one tz > 0 test in the pixel loop (the Z plane keeps pz)
