@@ -330,11 +330,12 @@ int youth_icp_track_frame(youth_icp_ctx* ctx, const int16_t* depth,
  * context's stream, and returns without waiting, so the next frame's copy
  * overlaps the aligns in flight.  At most YOUTH_TRACK_MAX_IN_FLIGHT frames
  * may be in flight (YOUTH_EINVAL otherwise): two suffice one frame at a
- * time; two micro-batches of two (youth_icp_track_submit_batch) use four.  youth_icp_track_collect waits for the OLDEST
+ * time; two micro-batches (youth_icp_track_submit_batch) use up to eight.
+ * youth_icp_track_collect waits for the OLDEST
  * submitted frame and returns exactly what youth_icp_track_frame would have
  * returned for it (status bits or a negative code, T_rel, *has_ref).
  * youth_icp_track_frame = submit + collect, with nothing in flight. */
-#define YOUTH_TRACK_MAX_IN_FLIGHT 4
+#define YOUTH_TRACK_MAX_IN_FLIGHT 8
 int youth_icp_track_submit(youth_icp_ctx* ctx, const int16_t* depth,
                            const double* T_init);
 int youth_icp_track_collect(youth_icp_ctx* ctx, double* T_rel, int* has_ref);
@@ -345,21 +346,23 @@ int youth_icp_track_pending(const youth_icp_ctx* ctx);
  * backlogged stream: the same as n_frames youth_icp_track_submit calls
  * (T_init identity), each frame collected by its own youth_icp_track_collect
  * with exactly the result youth_icp_track_frame gives, bit for bit.  When the
- * context holds a reference and has room (max_frames >= 4), the frames are
- * aligned by ONE cooperative launch in which pair i (frame i against frame
- * i - 1, frame -1 = the reference) runs on the single-pair plan and waits
- * for the pair before it to have prepped its target, if that grid fits
- * (youth_icp_track_set_batch's plan: it does; the default one at
- * 640x480 holds one pair); otherwise one launch per frame.  1 <= n_frames <= YOUTH_TRACK_MAX_BATCH, and at most
+ * context holds a reference and has room (max_frames >= 2 m for a chain of
+ * m frames), consecutive frames are aligned by ONE cooperative launch in
+ * which pair i (frame i against frame i - 1, frame -1 = the reference) runs
+ * on the single-pair plan and waits for the pair before it to have prepped
+ * its target, as many frames per launch as that plan's grids fit on the
+ * chip (youth_icp_track_set_batch(ctx, m) plans for m; the default plan at
+ * 640x480 holds one pair); the rest one launch per frame.
+ * 1 <= n_frames <= YOUTH_TRACK_MAX_BATCH, and at most
  * YOUTH_TRACK_MAX_IN_FLIGHT frames in flight afterwards (EINVAL). */
-#define YOUTH_TRACK_MAX_BATCH 2
+#define YOUTH_TRACK_MAX_BATCH 4
 int youth_icp_track_submit_batch(youth_icp_ctx* ctx, const int16_t* depth, int n_frames);
 
 /* Frames per submission youth_icp_track_host_sequence uses (1, default: one
  * launch per frame; up to YOUTH_TRACK_MAX_BATCH: micro-batches).  Batch mode
  * (> 1) plans the context's cooperative launches with the fewest source
- * pixels per lane that let that many pairs share one grid (640x480: 5 px
- * per lane, 120 workgroups per pair), so results stay bit-identical between
+ * pixels per lane that let that many pairs share one grid (640x480: 5, 8
+ * and 10 px per lane for 2, 3 and 4 frames), so results stay bit-identical between
  * batched and per-frame submission on that context (and within 1e-13 of the
  * oracle, like the default plan).
  * Returns the previous value or YOUTH_EINVAL. */
@@ -420,8 +423,9 @@ int youth_slam_get_pose(int index, uint32_t* timestamp, double* T_wc);
 /* Block until the ingest queue is empty and the worker is idle, or
  * timeout_ms elapses.  Returns 1 when drained, 0 on timeout / not running. */
 int youth_slam_wait_idle(int timeout_ms);
-/* Frames the worker has tracked in micro-batches of two since the module
- * started (YOUTH_SLAM_TRACK_BATCH=2 with a backlogged queue; 0 otherwise). */
+/* Frames the worker has submitted in micro-batches that ran as chained
+ * launches since the module started (YOUTH_SLAM_TRACK_BATCH=m >= 2 with a
+ * backlogged queue; 0 otherwise). */
 long long youth_slam_batched_frames(void);
 /* Block until the module stops (used by algorithmModule). */
 void youth_slam_wait_stopped(void);

@@ -2355,7 +2355,7 @@ struct youth_icp_ctx {
         hipEvent_t ev = nullptr;       // the one of the two recorded for this submission
         int has_ref = 0;
     } trk[kTrackDepth];
-    int trk_dslot_last[4] = {-1, -1, -1, -1};  // trk[] entry of the last launch that read depth slot d
+    int trk_dslot_last[2 * YOUTH_TRACK_MAX_BATCH];  // trk[] entry of the last launch that read depth slot d (-1: none)
     int trk_prev_d0 = -1;                       // first depth slot of the last launch
     int trk_head = 0, trk_n = 0;       // oldest in-flight submission, count in flight
 
@@ -3047,6 +3047,7 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         return nullptr;
     }
     auto* c = new youth_icp_ctx();
+    for (int& d : c->trk_dslot_last) d = -1;
     c->device = device;
     c->W = W;
     c->H = H;
@@ -3698,19 +3699,27 @@ static int ensure_track(youth_icp_ctx* c)
     return YOUTH_OK;
 }
 
-// Depth slots of the tracker (device staging of host frames): 4 when the
-// context has room (a micro-batch takes two consecutive ones, the other half
-// stays with the launch before), else 2.  Record slots: 3 (a micro-batch
-// preps two new frames beside the reference), else 2.
-static int trk_depth_slots(const youth_icp_ctx* c) { return c->max_frames >= 4 ? 4 : 2; }
-static int trk_record_slots(const youth_icp_ctx* c) { return c->max_frames >= 3 ? 3 : 2; }
+// Depth slots of the tracker (device staging of host frames): two halves of
+// B slots (B = the largest micro-batch the context has room for: a launch
+// takes consecutive slots of one half, the other half stays with the launch
+// before), or 2 (one frame per launch).  Record slots: B + 1 (a micro-batch
+// preps its B new frames beside the reference), at least 2.
+static int trk_half(const youth_icp_ctx* c)
+{
+    return std::max(1, std::min(kCoopMaxChain, c->max_frames / 2));
+}
+static int trk_depth_slots(const youth_icp_ctx* c) { return 2 * trk_half(c); }
+static int trk_record_slots(const youth_icp_ctx* c)
+{
+    return std::max(2, std::min(kCoopMaxChain + 1, c->max_frames));
+}
 
 // Whether m consecutive frames can be aligned as one k_icp_coop micro-batch:
 // every pair on the single-pair plan (bit-identical to track_frame), the m
 // grids co-resident, room for the slots.
 static bool trk_chain_fits(const youth_icp_ctx* c, int m)
 {
-    if (m < 2 || m > kCoopMaxChain || trk_depth_slots(c) < 2 * m || trk_record_slots(c) < m + 1 ||
+    if (m < 2 || m > kCoopMaxChain || m > trk_half(c) || trk_record_slots(c) < m + 1 ||
         c->prm.iters <= 0 || c->coop_refuse)
         return false;
     int npx = 0, G = 0;
@@ -3733,15 +3742,12 @@ static int track_submit_frames(youth_icp_ctx* c, const int16_t* depth, int m,
     hipStream_t s = c->stream;
     const size_t N = c->N;
     const int nds = trk_depth_slots(c), nrs = trk_record_slots(c);
-    // depth slots: the half (or slot) the previous launch did not use
-    int d0;
-    if (nds == 4)
-        d0 = c->trk_prev_d0 >= 2 || c->trk_prev_d0 < 0 ? 0 : 2;
-    else
-        d0 = c->trk_prev_d0 == 0 ? 1 : 0;
+    // depth slots: the half the previous launch did not use
+    const int half = nds / 2;
+    const int d0 = c->trk_prev_d0 >= half || c->trk_prev_d0 < 0 ? 0 : half;
     // record slots for the new frames: the first m that are not the reference
     const int ref = c->track_ref;
-    int rs[kCoopMaxChain] = {0, 0};
+    int rs[kCoopMaxChain] = {};
     for (int r = 0, k = 0; r < nrs && k < m; ++r)
         if (r != ref) rs[k++] = r;
     int qi[kCoopMaxChain];
@@ -3850,12 +3856,13 @@ int youth_icp_track_submit_batch(youth_icp_ctx* c, const int16_t* depth, int n_f
         if (rc) return rc;
         done = 1;
     }
-    const int rest = n_frames - done;
-    if (rest >= 2 && trk_chain_fits(c, rest))
-        return track_submit_frames(c, depth + (size_t)done * N, rest, nullptr);
-    for (int i = done; i < n_frames; ++i) {  // one launch per frame
-        rc = track_submit_frames(c, depth + (size_t)i * N, 1, nullptr);
+    // the rest in the longest chains that fit, else one launch per frame
+    while (done < n_frames) {
+        int m = n_frames - done;
+        while (m > 1 && !trk_chain_fits(c, m)) --m;
+        rc = track_submit_frames(c, depth + (size_t)done * N, m, nullptr);
         if (rc) return rc;
+        done += m;
     }
     return YOUTH_OK;
 }

@@ -18,6 +18,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -200,10 +201,11 @@ youth_intrinsics intrinsics_for(int w, int h)
 // while the host records k-1's pose and pops k+1.  A frame's pose reaches
 // the trajectory when the next frame is submitted or the queue runs empty
 // (the worker stays busy until then: youth_slam_wait_idle).
-// YOUTH_SLAM_TRACK_BATCH=2 (opt-in, for backlogged queues such as a .bin
-// replay): when a second frame of the same size is already queued, the two
-// are tracked as one micro-batch (youth_icp_track_submit_batch), two
-// submissions in flight; every frame then runs on the batch plan, so a pose
+// YOUTH_SLAM_TRACK_BATCH=m, 2 <= m <= YOUTH_TRACK_MAX_BATCH (opt-in, for
+// backlogged queues such as a .bin replay): frames of the same size already
+// queued behind the popped one (up to m in all) are tracked as one
+// micro-batch (youth_icp_track_submit_batch), two submissions in flight;
+// every frame then runs on the batch plan, so a pose
 // does not depend on whether its frame was batched.
 void worker_main(int device)
 {
@@ -211,10 +213,10 @@ void worker_main(int device)
     youth_icp_ctx* ctx = nullptr;
     int cw = 0, ch = 0;
     const char* eb = getenv("YOUTH_SLAM_TRACK_BATCH");
-    const int batch = eb && atoi(eb) >= 2 ? 2 : 1;
+    const int batch = eb ? std::max(1, std::min(atoi(eb), YOUTH_TRACK_MAX_BATCH)) : 1;
     const size_t kMaxFrame = (size_t)4096 * 4096;
     std::vector<int16_t> buf;
-    bool held = false;  // a popped frame not yet submitted, at buf[kMaxFrame]
+    bool held = false;  // a popped frame not yet submitted, at buf[batch kMaxFrame]
     int held_w = 0, held_h = 0;
     uint32_t held_ts = 0;
     double T_w_ref[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
@@ -257,13 +259,14 @@ void worker_main(int device)
         g_last_points = pr0.npts;
     };
     while (g_process.load()) {
-        if (buf.empty()) buf.resize(kMaxFrame * batch);
+        if (buf.empty()) buf.resize(kMaxFrame * (batch > 1 ? batch + 1 : 1));
+        int16_t* const scratch = buf.data() + kMaxFrame * batch;  // batch > 1 only
         int w = 0, h = 0;
         uint32_t ts = 0;
         g_busy.store(true);
         int got = 1;
         if (held) {
-            memmove(buf.data(), buf.data() + kMaxFrame, (size_t)held_w * held_h * sizeof(int16_t));
+            memmove(buf.data(), scratch, (size_t)held_w * held_h * sizeof(int16_t));
             w = held_w;
             h = held_h;
             ts = held_ts;
@@ -306,42 +309,42 @@ void worker_main(int device)
             for (size_t i = 0; i < N; ++i) n += d[i] > 0;
             return n;
         };
-        // micro-batch: a second frame of this size already waiting (one of
-        // another size, or of a sequence reset since, is held for the next
-        // round)
+        // micro-batch: frames of this size already waiting, up to `batch`
+        // in all (one of another size, or of a sequence reset since, is held
+        // for the next round)
         int m = 1;
-        uint32_t ts2 = 0;
-        if (batch > 1 && youth_queue_size(g_queue) > 0) {
+        uint32_t tss[YOUTH_TRACK_MAX_BATCH] = {};
+        tss[0] = ts;
+        while (m < batch && !held && youth_queue_size(g_queue) > 0) {
             int w2 = 0, h2 = 0;
-            if (youth_queue_pop(g_queue, buf.data() + kMaxFrame, kMaxFrame, &w2, &h2, &ts2) == 1) {
-                if (w2 == w && h2 == h && !g_reset.load()) {
-                    m = 2;
-                    memmove(buf.data() + N, buf.data() + kMaxFrame, N * sizeof(int16_t));
-                } else {
-                    held = true;
-                    held_w = w2;
-                    held_h = h2;
-                    held_ts = ts2;
-                }
+            uint32_t t2 = 0;
+            if (youth_queue_pop(g_queue, scratch, kMaxFrame, &w2, &h2, &t2) != 1) break;
+            if (w2 == w && h2 == h && !g_reset.load()) {
+                memmove(buf.data() + m * N, scratch, N * sizeof(int16_t));
+                tss[m++] = t2;
+            } else {
+                held = true;
+                held_w = w2;
+                held_h = h2;
+                held_ts = t2;
             }
         }
-        // two submissions in flight: frames, or micro-batches of two
+        // two submissions in flight: frames, or micro-batches
         while (!pend.empty() && (int)pend.size() + m > 2 * batch) finish_one(true);
         const long long chained0 = youth_icp_track_chained(ctx);
         const int rc = m == 1 ? youth_icp_track_submit(ctx, buf.data(), nullptr)
                               : youth_icp_track_submit_batch(ctx, buf.data(), m);
-        // frames that ran as one launch (a sequence's first frame is prepped alone)
-        g_batched.fetch_add(2 * (youth_icp_track_chained(ctx) - chained0));
+        // frames of a micro-batch that ran chained
+        if (youth_icp_track_chained(ctx) > chained0) g_batched.fetch_add(m);
         if (rc < 0) {
             fprintf(stderr, "youth_icp: tracking failed: %s\n", youth_icp_last_error());
-            // a micro-batch may have submitted its first frame before failing
+            // a micro-batch may have submitted its first frames before failing
             const int sent = youth_icp_track_pending(ctx) - (int)pend.size();
             for (int i = 0; i < sent && i < m; ++i)
-                pend.push_back(Pending{i ? ts2 : ts, count_points(buf.data() + i * N)});
+                pend.push_back(Pending{tss[i], count_points(buf.data() + i * N)});
             continue;
         }
-        pend.push_back(Pending{ts, count_points(buf.data())});
-        if (m == 2) pend.push_back(Pending{ts2, count_points(buf.data() + N)});
+        for (int i = 0; i < m; ++i) pend.push_back(Pending{tss[i], count_points(buf.data() + i * N)});
         if (batch == 1 && pend.size() == 2) finish_one(true);
     }
     while (ctx && !pend.empty()) finish_one(true);

@@ -959,7 +959,7 @@ def test_track_micro_batches_bit_identical():
             for k, ((Tg, sg, hg), (Tw, sw, hw)) in enumerate(zip(got, want)):
                 assert np.array_equal(Tg, Tw) and sg == sw and hg == hw, (batch_mode, k)
             with pytest.raises(youth_icp.IcpError):
-                ctx.track_submit_batch(frames[0:3])        # more than TRACK_MAX_BATCH
+                ctx.track_submit_batch(frames[0:youth_icp.TRACK_MAX_BATCH + 1])
             ctx.track_reset()
             ctx.track_submit_batch(frames[0:2])
             ctx.track_reset()                              # batch in flight
@@ -970,3 +970,42 @@ def test_track_micro_batches_bit_identical():
             Tb, stb = ctx.track_host_sequence(frames)
             assert np.array_equal(Tb, np.stack([w[0] for w in want[1:]]))
             assert np.array_equal(stb, np.array([w[1] for w in want[1:]], np.int32))
+
+
+@pytest.mark.parametrize("batch", [3, 4])
+def test_track_micro_batches_up_to_four(batch):
+    """Micro-batches of up to TRACK_MAX_BATCH frames (youth_icp_track_set_batch(
+    batch): the plan whose `batch` grids fit the chip at once, 8 / 10 px per
+    lane at 640x480): chains of 4, 3 and 2 frames, a submission longer than
+    the plan holds split into the longest chains that fit, and the library
+    loop with two submissions in flight, every frame bit-identical to
+    track_frame in the same plan and within 1e-5 of the oracle."""
+    frames, _ = youth_synth.sequence(7, 14)
+    with youth_icp.IcpContext(640, 480, 8) as ref:
+        ref.track_set_batch(batch)
+        want = [ref.track_frame(f) for f in frames]
+        plan = ref.get_plan()
+    assert plan["px_per_lane"] == {3: 8, 4: 10}[batch]
+    for k in range(1, len(frames)):
+        T64, _, sto, _ = oracle.align(frames[k], frames[k - 1])
+        assert want[k][1] == sto and _pose_err(want[k][0], T64) <= POSE_TOL
+    with youth_icp.IcpContext(640, 480, 2 * batch) as ctx:
+        ctx.track_set_batch(batch)
+        got = []
+        ctx.track_submit(frames[0])                        # the reference
+        k = 1
+        for m in (4, 3, 2, 1, 3):
+            ctx.track_submit_batch(frames[k:k + m])
+            got += [ctx.track_collect() for _ in range(m)]
+            k += m
+        while ctx.track_pending():
+            got.append(ctx.track_collect())
+        assert len(got) == len(frames)
+        # chains: 4 (batch 3: a chain of 3 + one frame); 3; 2; none; 3
+        assert ctx.track_chained() == 4, ctx.track_chained()
+        for i, ((Tg, sg, hg), (Tw, sw, hw)) in enumerate(zip(got, want)):
+            assert np.array_equal(Tg, Tw) and sg == sw and hg == hw, (batch, i)
+        ctx.track_reset()
+        Tb, stb = ctx.track_host_sequence(frames)
+        assert np.array_equal(Tb, np.stack([w[0] for w in want[1:]]))
+        assert np.array_equal(stb, np.array([w[1] for w in want[1:]], np.int32))

@@ -27,12 +27,13 @@ def drivers():
 TSAN_ENV = {"TSAN_OPTIONS": "halt_on_error=1 second_deadlock_stack=1"}
 ASAN_ENV = {"ASAN_OPTIONS": "detect_leaks=1 abort_on_error=0",
             "UBSAN_OPTIONS": "halt_on_error=1 print_stacktrace=1"}
-BATCH = {"YOUTH_SLAM_TRACK_BATCH": "2"}     # the worker's micro-batch mode
+BATCH2 = {"YOUTH_SLAM_TRACK_BATCH": "2"}    # the worker's micro-batch modes
+BATCH4 = {"YOUTH_SLAM_TRACK_BATCH": "4"}
 
 
 @pytest.mark.parametrize("kind,env", [
     ("tsan", TSAN_ENV), ("asan", ASAN_ENV),
-    ("tsan", {**TSAN_ENV, **BATCH}), ("asan", {**ASAN_ENV, **BATCH}),
+    ("tsan", {**TSAN_ENV, **BATCH4}), ("asan", {**ASAN_ENV, **BATCH2}),
 ], ids=["tsan", "asan", "tsan-batch", "asan-batch"])
 def test_host_threading_under_sanitizer(drivers, kind, env):
     r = subprocess.run([os.path.join(drivers, "driver_" + kind)], capture_output=True, text=True,

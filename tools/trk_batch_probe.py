@@ -2,9 +2,8 @@
 """Tracker micro-batch probe (run alone or under rocprofv3 --kernel-trace):
 the same host sequence through (a) the default plan, one launch per frame;
 (b) the batch plan (youth_icp_track_set_batch(2)) one launch per frame;
-(c) the batch plan in micro-batches of two frames through the library's C
-loop; (d) the same micro-batches from a Python loop with the host time of
-each submit and collect.  Prints frames/s of each."""
+(c) the batch plan in micro-batches of m = 2 .. TRACK_MAX_BATCH frames
+through the library's C loop.  Prints frames/s of each."""
 import os
 import sys
 import time
@@ -63,16 +62,13 @@ def run_py_batches(ctx, in_flight):
 a = youth_icp.IcpContext(640, 480, 4)
 run(a, False)
 print("default plan, per frame:", round(run(a, False)), a.get_plan(), flush=True)
-b = youth_icp.IcpContext(640, 480, 4)
-b.track_set_batch(2)
-run(b, False)
-print("batch plan, per frame:", round(run(b, False)), b.get_plan(), flush=True)
-run(b, True)
-print("batch plan, micro-batches (C loop):", [round(run(b, True)) for _ in range(5)], b.get_plan(),
-      "chained", b.track_chained(), flush=True)
-print("default plan, per frame (C loop):", [round(run(a, True)) for _ in range(5)], flush=True)
-for inf in (2, 4):
-    run_py_batches(b, inf)
-    r, s, c = run_py_batches(b, inf)
-    print(f"batch plan, micro-batches (Python, {inf} in flight): {round(r)} frames/s, "
-          f"submit {s:.1f} us, collect wait {c:.1f} us (medians)", flush=True)
+print("default plan, per frame (C loop):", [round(run(a, True)) for _ in range(3)], flush=True)
+for m in range(2, youth_icp.TRACK_MAX_BATCH + 1):
+    b = youth_icp.IcpContext(640, 480, 2 * m)
+    b.track_set_batch(m)
+    run(b, False)
+    print(f"batch plan {m}, per frame:", round(run(b, False)), b.get_plan(), flush=True)
+    run(b, True)
+    print(f"batch plan {m}, micro-batches (C loop):", [round(run(b, True)) for _ in range(3)],
+          "chained", b.track_chained(), flush=True)
+    b.close()
