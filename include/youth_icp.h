@@ -330,12 +330,12 @@ int youth_icp_track_frame(youth_icp_ctx* ctx, const int16_t* depth,
  * context's stream, and returns without waiting, so the next frame's copy
  * overlaps the aligns in flight.  At most YOUTH_TRACK_MAX_IN_FLIGHT frames
  * may be in flight (YOUTH_EINVAL otherwise): two suffice one frame at a
- * time; two micro-batches (youth_icp_track_submit_batch) use up to eight.
+ * time; two micro-batches (youth_icp_track_submit_batch) use up to 16.
  * youth_icp_track_collect waits for the OLDEST
  * submitted frame and returns exactly what youth_icp_track_frame would have
  * returned for it (status bits or a negative code, T_rel, *has_ref).
  * youth_icp_track_frame = submit + collect, with nothing in flight. */
-#define YOUTH_TRACK_MAX_IN_FLIGHT 8
+#define YOUTH_TRACK_MAX_IN_FLIGHT 16
 int youth_icp_track_submit(youth_icp_ctx* ctx, const int16_t* depth,
                            const double* T_init);
 int youth_icp_track_collect(youth_icp_ctx* ctx, double* T_rel, int* has_ref);
@@ -355,14 +355,14 @@ int youth_icp_track_pending(const youth_icp_ctx* ctx);
  * 640x480 holds one pair); the rest one launch per frame.
  * 1 <= n_frames <= YOUTH_TRACK_MAX_BATCH, and at most
  * YOUTH_TRACK_MAX_IN_FLIGHT frames in flight afterwards (EINVAL). */
-#define YOUTH_TRACK_MAX_BATCH 4
+#define YOUTH_TRACK_MAX_BATCH 8
 int youth_icp_track_submit_batch(youth_icp_ctx* ctx, const int16_t* depth, int n_frames);
 
 /* Frames per submission youth_icp_track_host_sequence uses (1, default: one
  * launch per frame; up to YOUTH_TRACK_MAX_BATCH: micro-batches).  Batch mode
  * (> 1) plans the context's cooperative launches with the fewest source
- * pixels per lane that let that many pairs share one grid (640x480: 5, 8
- * and 10 px per lane for 2, 3 and 4 frames), so results stay bit-identical between
+ * pixels per lane that let that many pairs share one grid (640x480: 5, 8,
+ * 10 and 19 px per lane for 2, 3, 4 and 8 frames), so results stay bit-identical between
  * batched and per-frame submission on that context (and within 1e-13 of the
  * oracle, like the default plan).
  * Returns the previous value or YOUTH_EINVAL. */

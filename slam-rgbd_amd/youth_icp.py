@@ -181,8 +181,8 @@ def _err(code: int) -> IcpError:
     return IcpError(code, (lib.youth_icp_last_error() or b"").decode())
 
 
-TRACK_MAX_IN_FLIGHT = 8   # YOUTH_TRACK_MAX_IN_FLIGHT (include/youth_icp.h)
-TRACK_MAX_BATCH = 4       # YOUTH_TRACK_MAX_BATCH
+TRACK_MAX_IN_FLIGHT = 16  # YOUTH_TRACK_MAX_IN_FLIGHT (include/youth_icp.h)
+TRACK_MAX_BATCH = 8       # YOUTH_TRACK_MAX_BATCH
 
 
 def _check(code: int) -> int:

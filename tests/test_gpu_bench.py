@@ -69,6 +69,9 @@ def test_bench_single_gpu_contract():
     assert d["c5"]["streamed"]["max_abs_diff_vs_batch_poses"] <= 1e-5
     assert d["c5"]["streamed"]["pipelined_equals_sync"]
     assert d["c5"]["streamed"]["batched_equals_sync"]
+    bs = d["c5"]["streamed"]["batched_by_size"]      # micro-batches of 2, 4 and 8 frames
+    assert set(bs) == {"2", "4", "8"} and all(v["value"] > 0 for v in bs.values())
+    assert all(v > 0 for v in d["c5"]["streamed"]["batched_launches"].values())
     assert d["kernel_path"]["kernel"].startswith("k_prep + k_icp")
     assert d["viewer_cloud"]["bit_exact_vs_cpu"]
     # spec a7/a8: the default is SURVEY §8a as worded; both arithmetics

@@ -420,9 +420,9 @@ def test_track_submit_collect_pipelined():
     result equals the synchronous track_frame sequence bit for bit, in any
     submit/collect interleaving; a reset with frames in flight starts a new
     sequence at the next submission; misuse is refused (EINVAL)."""
-    frames, _ = youth_synth.sequence(3, 9)
+    frames, _ = youth_synth.sequence(3, 11)
     with youth_icp.IcpContext(640, 480, 2) as ref:
-        want = [ref.track_frame(f) for f in frames]
+        want = [ref.track_frame(f) for f in frames[:9]]
     with youth_icp.IcpContext(640, 480, 2) as ctx:
         with pytest.raises(youth_icp.IcpError):
             ctx.track_collect()                              # nothing in flight
@@ -435,11 +435,11 @@ def test_track_submit_collect_pipelined():
                 k += 1
             else:
                 got.append(ctx.track_collect())
-        assert k == len(frames) and len(got) == len(frames) and ctx.track_pending() == 0
+        assert k == len(want) and len(got) == len(want) and ctx.track_pending() == 0
         for (Tg, sg, hg), (Tw, sw, hw) in zip(got, want):
             assert np.array_equal(Tg, Tw) and sg == sw and hg == hw
         D = youth_icp.TRACK_MAX_IN_FLIGHT
-        assert D == 4
+        assert D == 8
         for f in range(D):
             ctx.track_submit(frames[f])
         with pytest.raises(youth_icp.IcpError):
@@ -456,9 +456,9 @@ def test_track_submit_collect_pipelined():
         assert has and st == sto and _pose_err(T, T64) <= POSE_TOL
         # the library's own loop over a host sequence: the same results
         ctx.track_reset()
-        Tseq, stseq = ctx.track_host_sequence(frames)
-        assert Tseq.shape[0] == len(frames) - 1 and ctx.track_pending() == 0
-        for k in range(len(frames) - 1):
+        Tseq, stseq = ctx.track_host_sequence(frames[:9])
+        assert Tseq.shape[0] == len(want) - 1 and ctx.track_pending() == 0
+        for k in range(len(want) - 1):
             assert np.array_equal(Tseq[k], want[k + 1][0]) and stseq[k] == want[k + 1][1]
         Tmore, _ = ctx.track_host_sequence(frames[:2])       # continues from frame 8
         assert Tmore.shape[0] == 2
