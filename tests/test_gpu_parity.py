@@ -420,7 +420,7 @@ def test_track_submit_collect_pipelined():
     result equals the synchronous track_frame sequence bit for bit, in any
     submit/collect interleaving; a reset with frames in flight starts a new
     sequence at the next submission; misuse is refused (EINVAL)."""
-    frames, _ = youth_synth.sequence(3, 11)
+    frames, _ = youth_synth.sequence(3, 9 + youth_icp.TRACK_MAX_IN_FLIGHT)
     with youth_icp.IcpContext(640, 480, 2) as ref:
         want = [ref.track_frame(f) for f in frames[:9]]
     with youth_icp.IcpContext(640, 480, 2) as ctx:
@@ -439,7 +439,7 @@ def test_track_submit_collect_pipelined():
         for (Tg, sg, hg), (Tw, sw, hw) in zip(got, want):
             assert np.array_equal(Tg, Tw) and sg == sw and hg == hw
         D = youth_icp.TRACK_MAX_IN_FLIGHT
-        assert D == 8
+        assert D == 16
         for f in range(D):
             ctx.track_submit(frames[f])
         with pytest.raises(youth_icp.IcpError):
