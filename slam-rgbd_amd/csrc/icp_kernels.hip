@@ -1615,14 +1615,25 @@ struct IterState {
 // spreads the contended returning atomics over nq words (one per 128-B line):
 // MI355X_MICROARCH.md "dequeue": one head word pulled by 256+ CUs costs
 // ~3 us per dequeue, 8 per-XCD heads ~1.2 us.
-__device__ __forceinline__ int icp_dequeue(const IterState& is, int& q, int total)
+// Split in two so the first take's round trip can overlap other memory
+// traffic: icp_dequeue_issue takes a ticket from queue q's head (the atomic),
+// icp_dequeue_from decodes it, moving on to the next queues (synchronously)
+// while q is drained.
+__device__ __forceinline__ unsigned icp_dequeue_issue(const IterState& is, int q)
 {
+    return __hip_atomic_fetch_add(is.head + (kQHeads - kQHead) + q * kQHeadStride, 1u,
+                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int icp_dequeue_from(const IterState& is, int& q, unsigned first,
+                                                int total)
+{
+    unsigned t = first;
     for (int v = 0; v < is.nq; ++v) {
         const int npq = (is.n_pairs - q + is.nq - 1) / is.nq;
+        if (v > 0 && npq > 0) t = icp_dequeue_issue(is, q);
         if (npq > 0) {
             const int per = npq * is.nblk;
-            const int i = (int)__hip_atomic_fetch_add(is.head + (kQHeads - kQHead) + q * kQHeadStride,
-                                                      1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int i = (int)t;
             if (i < is.iters * per) {
                 const int k = i / per;
                 const int rem = i - k * per;
@@ -1634,6 +1645,10 @@ __device__ __forceinline__ int icp_dequeue(const IterState& is, int& q, int tota
         q = q + 1 == is.nq ? 0 : q + 1;
     }
     return total;
+}
+__device__ __forceinline__ int icp_dequeue(const IterState& is, int& q, int total)
+{
+    return icp_dequeue_from(is, q, icp_dequeue_issue(is, q), total);
 }
 
 constexpr unsigned kSpinMax = 1u << 23;  // x s_sleep(8) ~ seconds: a bound, never reached
@@ -1721,6 +1736,7 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
     __shared__ double sh_T64[12];
     __shared__ float sh_T32n[12];
     __shared__ int sh_item;
+    __shared__ int sh_next;
     __shared__ int sh_last;
     __shared__ float sh_T[12];
     const int N = W * H;
@@ -1732,8 +1748,11 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
     // thread 0's current queue: workgroups are dealt to the queues
     // round-robin (b and b + 8 share an XCD, so with 8 queues each XCD pulls
     // from its own head)
+    // (thread 1 keeps it: it dequeues the next item while wave 0 publishes)
     int myq = (int)(blockIdx.x % (unsigned)is.nq);
-    if (threadIdx.x == 0) sh_item = icp_claim(is, icp_dequeue(is, myq, total), total, per_iter, sh_T);
+    if (threadIdx.x == 1) sh_next = icp_dequeue(is, myq, total);
+    __syncthreads();
+    if (threadIdx.x == 0) sh_item = icp_claim(is, sh_next, total, per_iter, sh_T);
     __syncthreads();
     for (;;) {
         // LDS-broadcast values are wave-uniform: readfirstlane keeps them
@@ -1766,7 +1785,13 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
         __syncthreads();
 
         if (wave == 0) {
-            // ---- publish this chunk's partial, take the arrival ticket
+            // ---- publish this chunk's partial, take the arrival ticket; lane
+            // 1 takes the next item from the queue meanwhile (its round trip
+            // overlaps the stores' drain; the item is claimed, i.e. waited
+            // on, only after this workgroup has published: the queue stays
+            // deadlock-free)
+            unsigned first = 0u;
+            if (lane == 1) first = icp_dequeue_issue(is, myq);
             double sum = 0.0;
             if (lane < kPartStride) {
                 if (lane < kNeq)
@@ -1782,6 +1807,7 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
                     __HIP_MEMORY_SCOPE_AGENT);
                 sh_last = ticket == (unsigned)is.nblk - 1;
             }
+            if (lane == 1) sh_next = icp_dequeue_from(is, myq, first, total);
         }
         __syncthreads();
         if (__builtin_amdgcn_readfirstlane(sh_last)) {
@@ -1823,8 +1849,7 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
             }
         }
         // ---- next item (this workgroup has published: waiting is safe)
-        if (threadIdx.x == 0)
-            sh_item = icp_claim(is, icp_dequeue(is, myq, total), total, per_iter, sh_T);
+        if (threadIdx.x == 0) sh_item = icp_claim(is, sh_next, total, per_iter, sh_T);
         __syncthreads();
     }
 }
