@@ -372,8 +372,8 @@ int youth_icp_track_set_batch(youth_icp_ctx* ctx, int frames);
 long long youth_icp_track_chained(const youth_icp_ctx* ctx);
 
 /* A recorded host sequence (frames [n_frames][H][W], e.g. a .bin playback)
- * through the tracker, two frames in flight (with youth_icp_track_set_batch(2):
- * two micro-batches of two): the same results as
+ * through the tracker, two frames in flight (with youth_icp_track_set_batch(m):
+ * two micro-batches of m): the same results as
  * youth_icp_track_frame on each frame in order (continuing from the
  * reference the context holds).  T_rel [n][16] and status [n] (nullable)
  * receive the frames that had a reference, in order; returns how many, or a
