@@ -135,6 +135,64 @@ def test_assoc_bit_exact_every_iteration_640x480(spec):
 
 
 @pytest.mark.parametrize("spec", SPECS)
+def test_assoc_extreme_poses(spec):
+    """The projection's rare paths, given the same fp32 pose on both sides:
+    rotations up to 180 deg and translations along z of up to +-5 m put
+    source points behind the camera (P'_z <= 0), at P'_z next to 0 (the
+    quotient's range guard, the IEEE fallback) and far off the frame
+    (saturated coordinates, the row clamp into the record pad).  Indices
+    bit-exact, sums within rel 1e-11, match counts equal (k_reduce, which
+    shares the pixel code with k_icp and k_icp_coop)."""
+    oracle.set_spec(spec)
+    K = oracle.viewer_K(640, 480)
+    rng = np.random.default_rng(0xE47E)
+    src, dst, _ = youth_synth.pairs(77, 1)
+    Ts = []
+    with youth_icp.IcpContext(640, 480, 2, spec=spec) as ctx:
+        for draw in range(16):
+            axis = rng.normal(size=3)
+            axis /= np.linalg.norm(axis)
+            th = np.deg2rad(rng.uniform(60.0, 180.0))
+            t = np.r_[rng.uniform(-1.0, 1.0, 2), rng.uniform(-5.0, 5.0)]
+            if draw % 4 == 0:
+                t[2] = -float(np.median(src[src > 0])) / 1000.0   # the scene at the camera plane
+            Tr = oracle.se3_exp(np.r_[axis * th, t])
+            T32 = Tr[:3].astype(np.float32)
+            g_idx, g_neq = ctx.reduce(src[0], dst[0], T32)
+            o_idx = oracle.associate(src[0], dst[0], T32, K)
+            assert np.array_equal(g_idx, o_idx), draw
+            o_neq = oracle.reduce(src[0], dst[0], T32, K)
+            assert g_neq[28] == o_neq[28], draw
+            np.testing.assert_allclose(g_neq, o_neq, rtol=1e-11, atol=1e-9, err_msg=str(draw))
+            Ts.append(Tr)
+    # the first iteration's match count from the same initial poses through
+    # the cooperative kernel (one pair per call) and the persistent one (4
+    # pairs, YOUTH_ICP_NO_COOP): the same pixel code with the other match
+    # gate (masked normal / skipped update) and per-wave counts
+    want = [int(oracle.align(src[0], dst[0], iters=1, T_init=T)[3][0, 0]) for T in Ts]
+    ds = torch.from_numpy(np.stack([src[0]] * 4)).cuda()
+    dd = torch.from_numpy(np.stack([dst[0]] * 4)).cuda()
+    torch.cuda.synchronize()
+    with youth_icp.IcpContext(640, 480, 4, iters=1, spec=spec) as ctx:
+        for draw, T in enumerate(Ts):
+            ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), 1, T_init=T[None])
+            assert ctx.get_plan()["kernel"] == "k_icp_coop"
+            cnt, _ = ctx.get_stats(1, 1)
+            assert int(cnt[0, 0]) == want[draw], draw
+    os.environ["YOUTH_ICP_NO_COOP"] = "1"
+    try:
+        with youth_icp.IcpContext(640, 480, 4, iters=1, spec=spec) as ctx:
+            for d0 in range(0, len(Ts), 4):
+                ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), 4,
+                                       T_init=np.stack(Ts[d0:d0 + 4]))
+                assert ctx.get_plan()["kernel"].startswith("k_prep + k_icp")
+                cnt, _ = ctx.get_stats(4, 1)
+                assert [int(v) for v in cnt[:, 0]] == want[d0:d0 + 4], d0
+    finally:
+        del os.environ["YOUTH_ICP_NO_COOP"]
+
+
+@pytest.mark.parametrize("spec", SPECS)
 @pytest.mark.parametrize("W,H,iters,n", [(640, 480, 10, 1), (640, 480, 10, 8),
                                          (640, 480, 10, 64), (1280, 960, 20, 1),
                                          (1280, 960, 20, 2)])
