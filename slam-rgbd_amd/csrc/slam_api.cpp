@@ -216,7 +216,10 @@ void worker_main(int device)
     const int batch = eb ? std::max(1, std::min(atoi(eb), YOUTH_TRACK_MAX_BATCH)) : 1;
     const size_t kMaxFrame = (size_t)4096 * 4096;
     std::vector<int16_t> buf;
-    bool held = false;  // a popped frame not yet submitted, at buf[batch kMaxFrame]
+    // one kMaxFrame buffer: the popped frame at 0, a micro-batch's further
+    // frames at m N, and past them the pop target for the next one
+    bool held = false;  // a popped frame not yet submitted, at buf[held_off]
+    size_t held_off = 0;
     int held_w = 0, held_h = 0;
     uint32_t held_ts = 0;
     double T_w_ref[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
@@ -259,14 +262,13 @@ void worker_main(int device)
         g_last_points = pr0.npts;
     };
     while (g_process.load()) {
-        if (buf.empty()) buf.resize(kMaxFrame * (batch > 1 ? batch + 1 : 1));
-        int16_t* const scratch = buf.data() + kMaxFrame * batch;  // batch > 1 only
+        if (buf.empty()) buf.resize(kMaxFrame);
         int w = 0, h = 0;
         uint32_t ts = 0;
         g_busy.store(true);
         int got = 1;
         if (held) {
-            memmove(buf.data(), scratch, (size_t)held_w * held_h * sizeof(int16_t));
+            memmove(buf.data(), buf.data() + held_off, (size_t)held_w * held_h * sizeof(int16_t));
             w = held_w;
             h = held_h;
             ts = held_ts;
@@ -315,15 +317,20 @@ void worker_main(int device)
         int m = 1;
         uint32_t tss[YOUTH_TRACK_MAX_BATCH] = {};
         tss[0] = ts;
-        while (m < batch && !held && youth_queue_size(g_queue) > 0) {
+        const int mmax = (int)std::max<size_t>(1, std::min<size_t>(batch, kMaxFrame / N - 1));
+        int16_t* const scratch = buf.data() + (size_t)mmax * N;  // >= N values left
+        while (m < mmax && !held && youth_queue_size(g_queue) > 0) {
             int w2 = 0, h2 = 0;
             uint32_t t2 = 0;
-            if (youth_queue_pop(g_queue, scratch, kMaxFrame, &w2, &h2, &t2) != 1) break;
+            // a larger frame does not fit and stays queued for the next round
+            if (youth_queue_pop(g_queue, scratch, kMaxFrame - (size_t)mmax * N, &w2, &h2, &t2) != 1)
+                break;
             if (w2 == w && h2 == h && !g_reset.load()) {
                 memmove(buf.data() + m * N, scratch, N * sizeof(int16_t));
                 tss[m++] = t2;
             } else {
                 held = true;
+                held_off = (size_t)mmax * N;
                 held_w = w2;
                 held_h = h2;
                 held_ts = t2;

@@ -503,13 +503,14 @@ def test_slam_api_end_to_end():
     assert youth_icp.processSlamFrame(frames[0], None, 640, 480, 0) == 0
 
 
-def test_slam_worker_micro_batches(monkeypatch):
-    """YOUTH_SLAM_TRACK_BATCH=2: a backlogged queue (9 frames pushed at once,
+@pytest.mark.parametrize("batch", [2, 8])
+def test_slam_worker_micro_batches(monkeypatch, batch):
+    """YOUTH_SLAM_TRACK_BATCH=m: a backlogged queue (9 frames pushed at once,
     under the reference's drop threshold of 10) is tracked in micro-batches
-    of two.  Every pose is the one the batch plan gives frame by frame
+    of up to m.  Every pose is the one the batch plan gives frame by frame
     (composition aside: world poses within 1e-12 of the prefix product of
     the context's relative poses) and within 1e-5 of the oracle's."""
-    monkeypatch.setenv("YOUTH_SLAM_TRACK_BATCH", "2")
+    monkeypatch.setenv("YOUTH_SLAM_TRACK_BATCH", str(batch))
     F = 9
     frames, _ = youth_synth.sequence(0, F)
     youth_icp.initSlamModule(os.path.join(GOLDEN, "astra_camera.yaml"), "ORBvoc.txt")
@@ -524,8 +525,8 @@ def test_slam_worker_micro_batches(monkeypatch):
     assert list(ts) == [100 + k for k in range(F)]
     assert batched >= 2, batched
     K = youth_icp.parse_camera_yaml(os.path.join(GOLDEN, "astra_camera.yaml"))[0]
-    with youth_icp.IcpContext(640, 480, 4, K=K) as ctx:
-        ctx.track_set_batch(2)
+    with youth_icp.IcpContext(640, 480, 2 * batch, K=K) as ctx:
+        ctx.track_set_batch(batch)
         rel = [ctx.track_frame(f)[0] for f in frames][1:]
     acc, acc_o = np.eye(4), np.eye(4)
     assert np.array_equal(T[0], acc)
