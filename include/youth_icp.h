@@ -334,7 +334,10 @@ int youth_icp_track_frame(youth_icp_ctx* ctx, const int16_t* depth,
  * youth_icp_track_collect waits for the OLDEST
  * submitted frame and returns exactly what youth_icp_track_frame would have
  * returned for it (status bits or a negative code, T_rel, *has_ref).
- * youth_icp_track_frame = submit + collect, with nothing in flight. */
+ * youth_icp_track_frame = submit + collect, with nothing in flight.
+ * The first tracking call of a context pins YOUTH_TRACK_MAX_IN_FLIGHT
+ * staging frames of host memory (W x H x 2 bytes each: 9.8 MB at 640x480),
+ * freed by youth_icp_destroy. */
 #define YOUTH_TRACK_MAX_IN_FLIGHT 16
 int youth_icp_track_submit(youth_icp_ctx* ctx, const int16_t* depth,
                            const double* T_init);
