@@ -37,28 +37,6 @@ def run(ctx, batch_submit):
     return n / (time.perf_counter() - t0)
 
 
-def run_py_batches(ctx, in_flight):
-    """micro-batches from Python; returns (frames/s, median submit us,
-    median collect-wait us)"""
-    ctx.track_reset()
-    ts, tc = [], []
-    t0 = time.perf_counter()
-    ctx.track_submit(frames[0])
-    for f in range(1, n, 2):
-        m = min(2, n - f)
-        while ctx.track_pending() + m > in_flight:
-            a = time.perf_counter()
-            ctx.track_collect()
-            tc.append(time.perf_counter() - a)
-        a = time.perf_counter()
-        ctx.track_submit_batch(frames[f:f + m])
-        ts.append(time.perf_counter() - a)
-    while ctx.track_pending():
-        ctx.track_collect()
-    rate = n / (time.perf_counter() - t0)
-    return rate, 1e6 * float(np.median(ts)), 1e6 * float(np.median(tc))
-
-
 a = youth_icp.IcpContext(640, 480, 4)
 run(a, False)
 print("default plan, per frame:", round(run(a, False)), a.get_plan(), flush=True)
