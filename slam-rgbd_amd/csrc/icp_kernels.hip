@@ -1279,9 +1279,9 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
         const_cast<float4*>(rec), (short)0, rec_bytes, 0x00020000);
     // (u0, v0) of pixel i advance incrementally (no integer division per
     // step); with kAligned (W % 4 == 0, i % 4 == 0) a lane's four pixels
-    // share one row.  Conditions combine with '&' so the compiler emits
-    // selects, not exec-mask branches; unmatched pixels gather record 0 and
-    // are masked.
+    // share one row.  The match conditions are lane masks (xform_project,
+    // match_accumulate), so the four gathers issue back to back; an
+    // unmatched pixel's gather is dropped by its mask.
     const int stepV = kRedStep / W;
     const int stepU = kRedStep - stepV * W;
     int i = start + threadIdx.x * 4;
