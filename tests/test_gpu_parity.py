@@ -973,6 +973,31 @@ def test_track_micro_batches_bit_identical():
             assert np.array_equal(stb, np.array([w[1] for w in want[1:]], np.int32))
 
 
+def test_track_micro_batches_1280x960():
+    """C3's frame size through the tracker in micro-batches of two (the plan
+    whose two grids fit the chip: 20 px per lane, 120 workgroups per pair,
+    123 KB of source LDS per workgroup): every frame bit-identical to
+    track_frame in the same plan, chained launches used, and within 1e-5 of
+    the oracle at 20 iterations."""
+    W, H, it = 1280, 960, 20
+    frames, _ = youth_synth.sequence(3, 7, W, H)
+    K = youth_icp.default_intrinsics(W, H)
+    with youth_icp.IcpContext(W, H, 4, K=K, iters=it) as ref:
+        ref.track_set_batch(2)
+        want = [ref.track_frame(f) for f in frames]
+        plan = ref.get_plan()
+    with youth_icp.IcpContext(W, H, 4, K=K, iters=it) as ctx:
+        ctx.track_set_batch(2)
+        Tb, stb = ctx.track_host_sequence(frames)
+        chained = ctx.track_chained()
+    assert chained >= 2, (chained, plan)
+    assert np.array_equal(Tb, np.stack([w[0] for w in want[1:]]))
+    assert np.array_equal(stb, np.array([w[1] for w in want[1:]], np.int32))
+    for k in (1, len(frames) - 1):
+        T64, _, sto, _ = oracle.align(frames[k], frames[k - 1], iters=it)
+        assert want[k][1] == sto and _pose_err(want[k][0], T64) <= POSE_TOL
+
+
 @pytest.mark.parametrize("batch", [3, 4])
 def test_track_micro_batches_up_to_four(batch):
     """Micro-batches of up to TRACK_MAX_BATCH frames (youth_icp_track_set_batch(
