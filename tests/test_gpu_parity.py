@@ -998,6 +998,33 @@ def test_track_micro_batches_1280x960():
         assert want[k][1] == sto and _pose_err(want[k][0], T64) <= POSE_TOL
 
 
+@pytest.mark.parametrize("spec", ["survey", "fma"])
+@pytest.mark.parametrize("W,H", [(97, 53), (160, 120)])
+def test_track_micro_batches_ragged_sizes(W, H, spec):
+    """Micro-batches of 4 at ragged frame sizes (narrow halo loads, partial
+    tiles, a few workgroups per pair) in both arithmetics: the library loop
+    bit-identical to track_frame in the same plan, every frame within 1e-5
+    of the oracle in that arithmetic."""
+    oracle.set_spec(spec)
+    try:
+        frames, _ = youth_synth.sequence(11, 9, W, H)
+        K = youth_icp.default_intrinsics(W, H)
+        with youth_icp.IcpContext(W, H, 8, K=K, spec=spec) as ref:
+            ref.track_set_batch(4)
+            want = [ref.track_frame(f) for f in frames]
+        with youth_icp.IcpContext(W, H, 8, K=K, spec=spec) as ctx:
+            ctx.track_set_batch(4)
+            Tb, stb = ctx.track_host_sequence(frames)
+            assert ctx.track_chained() >= 2
+        assert np.array_equal(Tb, np.stack([w[0] for w in want[1:]]))
+        assert np.array_equal(stb, np.array([w[1] for w in want[1:]], np.int32))
+        for k in range(1, len(frames)):
+            T64, _, sto, _ = oracle.align(frames[k], frames[k - 1])
+            assert want[k][1] == sto and _pose_err(want[k][0], T64) <= POSE_TOL, k
+    finally:
+        oracle.set_spec("survey")
+
+
 @pytest.mark.parametrize("batch", [3, 4])
 def test_track_micro_batches_up_to_four(batch):
     """Micro-batches of up to TRACK_MAX_BATCH frames (youth_icp_track_set_batch(
