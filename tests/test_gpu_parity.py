@@ -973,6 +973,63 @@ def test_track_micro_batches_bit_identical():
             assert np.array_equal(stb, np.array([w[1] for w in want[1:]], np.int32))
 
 
+def test_coop_launches_from_several_streams():
+    """Cooperative launches from three contexts at once, issued interleaved
+    from one host thread without syncs: two single-pair aligns on two torch
+    streams and a tracker in micro-batches of two on its own stream.  The
+    library orders a device's k_icp_coop grids across streams (coop_enqueue),
+    so none waits on a workgroup that cannot be resident: no timeout, and
+    every result equals the one each context gives alone, bit for bit."""
+    import torch
+    N = 640 * 480
+    src, dst, _ = youth_synth.pairs(40, 2)
+    frames, _ = youth_synth.sequence(21, 9)
+    ds, dd = torch.from_numpy(src).cuda(), torch.from_numpy(dst).cuda()
+    torch.cuda.synchronize()
+    want = []
+    for p in range(2):
+        with youth_icp.IcpContext(640, 480, 2) as ctx:
+            ctx.align_pairs_device(ds.data_ptr() + 2 * N * p, dd.data_ptr() + 2 * N * p, 1)
+            want.append(ctx.get_poses(1)[1][0])
+    with youth_icp.IcpContext(640, 480, 4) as ref:
+        ref.track_set_batch(2)
+        want_trk = [ref.track_frame(f) for f in frames]
+    reps = 24
+    outs = [torch.zeros((reps, 16), device="cuda") for _ in range(2)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    ctxs = [youth_icp.IcpContext(640, 480, 2) for _ in range(2)]
+    trk = youth_icp.IcpContext(640, 480, 4)
+    trk.track_set_batch(2)
+    got_trk = []
+    try:
+        trk.track_submit(frames[0])
+        f = 1
+        for r in range(reps):
+            for p in range(2):
+                ctxs[p].align_pairs_device(ds.data_ptr() + 2 * N * p, dd.data_ptr() + 2 * N * p,
+                                           1, d_T_out=outs[p][r].data_ptr(),
+                                           stream=streams[p].cuda_stream)
+            if f + 2 <= len(frames) and r % 3 == 0:
+                trk.track_submit_batch(frames[f:f + 2])
+                f += 2
+            while trk.track_pending() > 2:
+                got_trk.append(trk.track_collect())
+        while trk.track_pending():
+            got_trk.append(trk.track_collect())
+        torch.cuda.synchronize()
+        for p in range(2):
+            assert not ctxs[p].get_poses(1)[2].any()
+            rows = outs[p].cpu().numpy().reshape(reps, 4, 4)
+            for r in range(reps):
+                assert np.array_equal(rows[r][:3], want[p][:3]), (p, r)
+    finally:
+        for c in ctxs + [trk]:
+            c.close()
+    assert len(got_trk) == f
+    for (Tg, sg, hg), (Tw, sw, hw) in zip(got_trk, want_trk):
+        assert np.array_equal(Tg, Tw) and sg == sw and hg == hw
+
+
 def test_track_micro_batches_1280x960():
     """C3's frame size through the tracker in micro-batches of two (the plan
     whose two grids fit the chip: 20 px per lane, 120 workgroups per pair,
