@@ -1030,6 +1030,52 @@ def test_coop_launches_from_several_streams():
         assert np.array_equal(Tg, Tw) and sg == sw and hg == hw
 
 
+def test_coop_launches_from_host_threads():
+    """Four host threads, each with its own context and stream, align single
+    pairs concurrently (ctypes drops the GIL inside the library): the device's
+    cooperative launches are ordered under its lock from every thread, and
+    every thread gets the pose its pair gives alone, bit for bit."""
+    import threading
+    import torch
+    src, dst, _ = youth_synth.pairs(60, 4)
+    ds, dd = torch.from_numpy(src).cuda(), torch.from_numpy(dst).cuda()
+    torch.cuda.synchronize()
+    N = 640 * 480
+
+    def align(ctx, p, stream):
+        ctx.align_pairs_device(ds.data_ptr() + 2 * N * p, dd.data_ptr() + 2 * N * p, 1,
+                               stream=stream.cuda_stream)
+        stream.synchronize()
+        T64, _, st = ctx.get_poses(1)
+        return T64[0], int(st[0])
+
+    want = []
+    s0 = torch.cuda.Stream()
+    for p in range(4):
+        with youth_icp.IcpContext(640, 480, 2) as ctx:
+            want.append(align(ctx, p, s0))
+    errors, results = [], [None] * 4
+
+    def worker(p):
+        try:
+            stream = torch.cuda.Stream()
+            with youth_icp.IcpContext(640, 480, 2) as ctx:
+                results[p] = [align(ctx, p, stream) for _ in range(12)]
+        except Exception as e:  # reported by the main thread
+            errors.append(f"{p}: {e!r}")
+
+    threads = [threading.Thread(target=worker, args=(p,)) for p in range(4)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in threads) and not errors, errors
+    for p in range(4):
+        assert want[p][1] == 0 and len(results[p]) == 12
+        for T, st in results[p]:
+            assert st == 0 and np.array_equal(T, want[p][0]), p
+
+
 def test_track_micro_batches_1280x960():
     """C3's frame size through the tracker in micro-batches of two (the plan
     whose two grids fit the chip: 20 px per lane, 120 workgroups per pair,
