@@ -1159,6 +1159,11 @@ def test_track_micro_batches_up_to_four(batch):
         assert len(got) == len(frames)
         # chains: 4 (batch 3: a chain of 3 + one frame); 3; 2; none; 3
         assert ctx.track_chained() == 4, ctx.track_chained()
+        for bad in (0, youth_icp.TRACK_MAX_BATCH + 1):
+            with pytest.raises(youth_icp.IcpError):
+                ctx.track_set_batch(bad)
+            with pytest.raises(youth_icp.IcpError):
+                ctx.track_submit_batch(frames[:bad] if bad else frames[:0])
         for i, ((Tg, sg, hg), (Tw, sw, hw)) in enumerate(zip(got, want)):
             assert np.array_equal(Tg, Tw) and sg == sw and hg == hw, (batch, i)
         ctx.track_reset()
