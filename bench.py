@@ -286,19 +286,34 @@ def roofline_icp(a, kt, n_pairs, W, H):
     return out
 
 
-def roofline_prep(kt, n_frames, W, H):
+def roofline_prep(a, kt, n_frames, W, H):
     """k_prep (target records, once per align): 2 B depth in + 16 B record out
-    per target pixel, HIP events over a short pass after the timed region."""
+    per target pixel, HIP events over a short pass after the timed region.
+    `traffic` (PMC HBM bytes: the halo re-reads show up here)
+    and the VALU issue fraction come from the committed PMC pass of the same
+    kernel source, as for k_icp."""
     ms, launches = kt["k_prep"]
     if launches == 0:
         return None
     avg = ms / launches
-    alg = PREP_BYTES_PER_PX * n_frames * W * H
+    px = n_frames * W * H
+    alg = PREP_BYTES_PER_PX * px
     ach = alg / (avg * 1e-3) / 1e9
-    return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": ach / HBM_PEAK_GBS, "kernel": "k_prep", "algorithmic_bytes_per_launch": alg,
-            "algorithmic_model": "18 B per target pixel (depth 2 in + record 16 out)",
-            "avg_launch_ms": avg, "launches": launches}
+    out = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": ach / HBM_PEAK_GBS, "kernel": "k_prep", "algorithmic_bytes_per_launch": alg,
+           "algorithmic_model": "18 B per target pixel (depth 2 in + record 16 out)",
+           "avg_launch_ms": avg, "launches": launches}
+    tj, src = load_pmc(a, W, H)
+    if tj and "k_prep_bytes_per_px" in tj:
+        traffic = tj["k_prep_bytes_per_px"] * px
+        out.update({"traffic": traffic, "traffic_source": src,
+                    "traffic_frac": traffic / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                    "traffic_over_algorithmic": traffic / alg})
+    if tj and "k_prep_valu_busy_frac" in tj:
+        acc = tj["k_prep_valu_account"]
+        out["valu_issue_frac"] = tj["k_prep_valu_busy_frac"]
+        out["valu_busy_frac_range"] = [acc["busy_frac_other_at_2_4_cycles"], acc["busy_frac"]]
+    return out
 
 
 def pose_err(Ta, Tb):
@@ -390,7 +405,7 @@ def run_pairs(R):
     }
     result["window_rates"] = [n_glob * a.steps / s for s in spread]
     result["roofline"] = roofline_icp(a, kt, n, W, H)
-    result["roofline_prep"] = roofline_prep(kt, n, W, H)
+    result["roofline_prep"] = roofline_prep(a, kt, n, W, H)
     result["kernel_ms_per_step"] = {"k_icp": kt["k_icp"][0] / max(kt["k_icp"][1], 1),
                                     "k_prep": kt["k_prep"][0] / max(kt["prep_pass_steps"], 1)}
     spins, waited = ctx.get_sched_stats()   # last align: persistent-kernel pose waits

@@ -52,6 +52,8 @@ def test_bench_single_gpu_contract():
     assert rf["iterations_per_launch"] == 10
     rp = d["roofline_prep"]
     assert rp["kernel"] == "k_prep" and 0 < rp["frac"] < 1.0
+    if rp.get("traffic_source", "").startswith("profiles/"):    # PMC pass of this source
+        assert 1.0 <= rp["traffic_over_algorithmic"] < 1.5 and 0 < rp["valu_issue_frac"] < 1.0
     cb = d["cpu_baseline"]
     for k in ("value", "unit", "cores", "kind", "sample", "threads_share", "threads_all"):
         assert k in cb, k

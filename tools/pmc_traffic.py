@@ -33,6 +33,36 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_summary import summarize  # noqa: E402
 
 
+def valu_account(r, simds, costs_path, root_dir):
+    """VALU issue account of one kernel's PMC row: instruction
+    classes from the SQ_INSTS_VALU_* counters x their measured issue cost in
+    SIMD-cycles (tools/valu_costs.py over tools/valu_rate, the same GRBM
+    normalisation), against the SIMD-cycles of the launch.  "other" =
+    SQ_INSTS_VALU minus the classified ones (v_cmp, v_cndmask, v_mov,
+    permlane / readlane / DPP); its cost is bracketed by the 4.3-cycle
+    compare/select forms and the 2.4-cycle moves.  None without the counters."""
+    cls = ["ADD_F32", "MUL_F32", "FMA_F32", "TRANS_F32", "FMA_F64", "ADD_F64", "MUL_F64", "CVT",
+           "INT32", "INT64"]
+    if not (os.path.exists(costs_path) and all(f"SQ_INSTS_VALU_{c}" in r for c in cls) and
+            "GRBM_GUI_ACTIVE" in r and "SQ_INSTS_VALU" in r):
+        return None
+    cost = json.load(open(costs_path))["simd_cycles_per_wave_instruction"]
+    avail = simds * r["GRBM_GUI_ACTIVE"] / N_XCD
+    counts = {c: r[f"SQ_INSTS_VALU_{c}"] for c in cls}
+    counts["other"] = max(0.0, r["SQ_INSTS_VALU"] - sum(counts.values()))
+    cyc = {c: counts[c] * cost[c]["cycles"] for c in counts}
+    lo = sum(cyc.values()) - cyc["other"] + counts["other"] * cost["other_2cycle"]["cycles"]
+    return {
+        "simd_cycles_available": avail,
+        "instructions_by_class": counts,
+        "issue_cycles_by_class": cyc,
+        "issue_cycles": sum(cyc.values()),
+        "busy_frac": sum(cyc.values()) / avail,
+        "busy_frac_other_at_2_4_cycles": lo / avail,
+        "cost_source": os.path.relpath(costs_path, root_dir),
+    }
+
+
 def main():
     root, out, pairs, W, H = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), \
         int(sys.argv[5])
@@ -88,37 +118,12 @@ def main():
         if durs:
             avg_ns = sum(durs) / len(durs)
             doc["effective_clock_ghz"] = cyc / avg_ns
-    # VALU issue account: instruction classes from the
-    # SQ_INSTS_VALU_* counters x their measured issue cost in SIMD-cycles
-    # (tools/valu_costs.py over tools/valu_rate, the same GRBM normalisation),
-    # against the SIMD-cycles of the launch.  "other" = SQ_INSTS_VALU minus
-    # the classified ones (v_cmp, v_cndmask, v_mov, permlane / readlane / DPP);
-    # its cost is bracketed by the 4.3-cycle compare/select forms and the
-    # 2.4-cycle moves.
-    costs_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                              "profiles", "r03", "valu_costs.json")
-    cls = ["ADD_F32", "MUL_F32", "FMA_F32", "TRANS_F32", "FMA_F64", "ADD_F64", "MUL_F64", "CVT",
-           "INT32", "INT64"]
-    if os.path.exists(costs_path) and all(f"SQ_INSTS_VALU_{c}" in r for c in cls) and \
-            "GRBM_GUI_ACTIVE" in r and "SQ_INSTS_VALU" in r:
-        cost = json.load(open(costs_path))["simd_cycles_per_wave_instruction"]
-        simds = doc.get("simds", 1024)
-        avail = simds * r["GRBM_GUI_ACTIVE"] / N_XCD
-        counts = {c: r[f"SQ_INSTS_VALU_{c}"] for c in cls}
-        counts["other"] = max(0.0, r["SQ_INSTS_VALU"] - sum(counts.values()))
-        cyc = {c: counts[c] * cost[c]["cycles"] for c in counts}
-        lo = sum(cyc.values()) - cyc["other"] + counts["other"] * cost["other_2cycle"]["cycles"]
-        doc["valu_account"] = {
-            "simd_cycles_available": avail,
-            "instructions_by_class": counts,
-            "issue_cycles_by_class": cyc,
-            "issue_cycles": sum(cyc.values()),
-            "busy_frac": sum(cyc.values()) / avail,
-            "busy_frac_other_at_2_4_cycles": lo / avail,
-            "cost_source": os.path.relpath(costs_path, os.path.dirname(os.path.dirname(
-                os.path.abspath(__file__)))),
-        }
-        doc["valu_busy_frac"] = sum(cyc.values()) / avail
+    root_dir = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    costs_path = os.path.join(root_dir, "profiles", "r03", "valu_costs.json")
+    acc = valu_account(r, doc.get("simds", 1024), costs_path, root_dir)
+    if acc:
+        doc["valu_account"] = acc
+        doc["valu_busy_frac"] = acc["busy_frac"]
         doc["valu_busy_definition"] = ("sum over VALU classes of SQ_INSTS_VALU_<class> x its "
                                        "measured issue cost (SIMD-cycles, tools/valu_rate) / "
                                        "(SIMDs x GRBM_GUI_ACTIVE / 8 XCDs)")
@@ -132,6 +137,15 @@ def main():
         if m and "FETCH_SIZE" in res[m]:
             doc[k + "_hbm_bytes"] = 2.0 * res[m]["FETCH_SIZE"] * 1024 + \
                 res[m].get("WRITE_SIZE", 0.0) * 1024
+    # k_prep (one target frame per pair): bytes per target pixel and its VALU issue
+    m = next((x for x in res if x.startswith("k_prep")), None)
+    if m:
+        if "k_prep_hbm_bytes" in doc:
+            doc["k_prep_bytes_per_px"] = doc["k_prep_hbm_bytes"] / (pairs * W * H)
+        pacc = valu_account(res[m], doc.get("simds", 1024), costs_path, root_dir)
+        if pacc:
+            doc["k_prep_valu_account"] = pacc
+            doc["k_prep_valu_busy_frac"] = pacc["busy_frac"]
     json.dump(doc, open(out, "w"), indent=1)
     print(json.dumps(doc, indent=1))
 
