@@ -116,6 +116,34 @@ def test_bench_two_ranks_rehearsal(workload):
 
 
 @pytest.mark.parametrize("workload", ["pairs", "sequence"])
+def test_bench_three_ranks_uneven_shards(workload):
+    """Three ranks over gloo on one GPU with shards that do not divide evenly
+    (100 pairs: 34 + 33 + 33; a 61-frame sequence: 60 pairs, 20 per rank with
+    a 1-frame halo): the line's shape, every rank's timings, and bench.py's
+    own check that the gathered poses equal each rank's (it raises
+    otherwise).  Shards stay above 16 pairs, so no rank launches the
+    cooperative kernel (its grids assume one process per GPU)."""
+    env = dict(os.environ, YOUTH_BENCH_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus",
+           "3", "--steps", "3", "--warmup", "1", "--windows", "1", "--workload", workload,
+           "--global-pairs", "100", "--frames", "61"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 3 and d["value"] > 0 and d["scaling"] == "strong"
+    if workload == "pairs":
+        assert d["config"]["global_pairs"] == 100
+    else:
+        assert d["config"]["pairs"] == 60
+    rk = d["ranks"]
+    assert rk["rccl_world_size"] == 3 and rk["backend"] == "gloo"
+    for k in ("k_icp_ms", "k_prep_ms", "gather_ms"):
+        assert len(rk["per_rank_ms"][k]) == 3, k
+    assert min(rk["per_rank_ms"]["k_icp_ms"]) > 0
+
+
+@pytest.mark.parametrize("workload", ["pairs", "sequence"])
 def test_bench_rccl_gather_one_gpu(workload):
     """The RCCL path itself on hardware: one rank with the process group up
     (YOUTH_BENCH_DIST=1, backend nccl = RCCL): init_process_group(device_id=),
