@@ -1,4 +1,4 @@
-"""CPU tests of the N>1 path: world_size 2 over gloo (127.0.0.1).
+"""CPU tests of the N>1 path: world_size 2 and 3 over gloo (127.0.0.1).
 
 Covers the pair sharding (weak scaling, global seeds), the pose all-gather
 (rank order), the sequence sharding with its 1-frame halo, and rank 0's
@@ -58,8 +58,8 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(300)
-def test_world2_gloo_shards_and_gather():
-    world = 2
+@pytest.mark.parametrize("world", [2, 3])
+def test_world2_gloo_shards_and_gather(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -71,20 +71,26 @@ def test_world2_gloo_shards_and_gather():
         rank, allp, rng, rows, rep = q.get(timeout=240)
         res[rank] = (allp, rng, rows)
         assert rep["rccl_world_size"] == world and rep["backend"] == "gloo"
-        assert rep["per_rank_ms"]["k_icp_ms"] == [1.0, 2.0]
-        assert rep["per_rank_ms"]["k_prep_ms"] == [0.0, 0.1]
-        assert rep["per_rank_ms"]["gather_ms"] == [0.01, 0.01]
+        assert rep["per_rank_ms"]["k_icp_ms"] == [1.0 + r for r in range(world)]
+        assert np.allclose(rep["per_rank_ms"]["k_prep_ms"], [0.1 * r for r in range(world)])
+        assert rep["per_rank_ms"]["gather_ms"] == [0.01] * world
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     # every rank sees the same rank-ordered gather == the global pair list
-    _, _, T_all = youth_synth.pairs(0, 6, 64, 48)
+    _, _, T_all = youth_synth.pairs(0, 3 * world, 64, 48)
     for r in range(world):
-        assert np.array_equal(res[r][0], T_all.reshape(6, 16).astype(np.float32))
+        assert np.array_equal(res[r][0], T_all.reshape(3 * world, 16).astype(np.float32))
     # sequence shards tile the 8 pairs with a shared halo frame
-    assert res[0][1] == (0, 5) and res[1][1] == (4, 9)
+    if world == 2:
+        assert res[0][1] == (0, 5) and res[1][1] == (4, 9)
+    for r in range(1, world):
+        assert res[r][1][0] == res[r - 1][1][1] - 1          # one-frame halo
+    assert res[0][1][0] == 0 and res[world - 1][1][1] == 9
     rows = res[0][2]
-    assert rows.shape == (8, 16) and np.array_equal(rows, res[1][2])
+    assert rows.shape == (8, 16)
+    for r in range(1, world):
+        assert np.array_equal(rows, res[r][2])
     _, Twc = youth_synth.sequence(0, 9, 64, 48)
     traj = youth_dist.compose_trajectory(rows.reshape(8, 4, 4))
     assert np.allclose(traj, np.linalg.inv(Twc[0]) @ Twc, atol=1e-12)
