@@ -72,8 +72,12 @@ def parse():
                     help="pairs workload: steps in flight per rank; 2 = two contexts on two "
                          "streams, so step s+1's k_prep / k_icp fill step s's k_icp tail "
                          "(independent batches, each completed inside the timed region); "
-                         "0 = auto: 2 for shards of <= 96 pairs (N = 8's 64: +2 %), else 1 "
-                         "(512 / 128 pairs: -1 %; profiles/r03/ab_pipeline.txt)")
+                         "0 = auto: 2 for shards of <= 192 pairs, each k_icp on half the "
+                         "workgroup slots (--share; N = 8's 64 pairs: +4 %, N = 4's 128: "
+                         "+2 %), else 1 (256 pairs: neutral; profiles/r03/ab_share.txt)")
+    ap.add_argument("--share", type=int, default=0, choices=[0, 1, 2, 3, 4],
+                    help="pairs workload: k_icp slot share per context "
+                         "(youth_icp_set_concurrency); 0 = the steps in flight")
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
@@ -237,16 +241,19 @@ def load_pmc(a, W, H):
     return tj, os.path.relpath(a.traffic_json, ROOT)
 
 
-def roofline_icp(a, kt, n_pairs, W, H):
+def roofline_icp(a, kt, n_pairs, W, H, concurrent=1):
     """Roofline of the dominant kernel, k_icp (persistent: all iterations of
     an align in ONE launch).  `achieved` = the kernel's algorithmic bytes
     (18 B per pixel-iteration: 2 B source depth + one 16-B target record,
     DESIGN.md §3) x pixels x iterations per launch / the average launch
     duration from HIP events on the launch stream inside the timed region.
     `traffic` = PMC-measured HBM bytes per launch (same build); `survey_model`
-    = the same time against SURVEY §8d's 36 B/px model."""
+    = the same time against SURVEY §8d's 36 B/px model.  `concurrent` > 1:
+    that many launches run side by side, each on 1/concurrent of the
+    workgroup slots (youth_icp_set_concurrency), so the chip's rate is
+    concurrent x bytes per launch / launch duration."""
     ms, launches = kt["k_icp"]
-    avg = ms / max(launches, 1)
+    avg = ms / max(launches, 1) / concurrent  # chip time per launch
     ipl = max(1, round(a.steps * a.iters / max(launches, 1)))
     px = n_pairs * W * H * ipl
     alg = ICP_BYTES_PER_PX_ITER * px
@@ -260,7 +267,8 @@ def roofline_icp(a, kt, n_pairs, W, H):
         "algorithmic_bytes_per_launch": alg,
         "algorithmic_model": "18 B per pixel-iteration (src depth 2 + tgt record 16) x pairs x "
                              "W x H x iterations",
-        "avg_launch_ms": avg, "launches": launches, "iterations_per_launch": ipl,
+        "avg_launch_ms": avg * concurrent, "launches": launches, "iterations_per_launch": ipl,
+        "concurrent_launches": concurrent,
         "survey_model": {"bytes_per_px_iter": SURVEY_BYTES_PER_PX_ITER,
                          "achieved": SURVEY_BYTES_PER_PX_ITER * px / (avg * 1e-3) / 1e9,
                          "frac": SURVEY_BYTES_PER_PX_ITER * px / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS,
@@ -350,13 +358,18 @@ def run_pairs(R):
     host = [torch.zeros((n_glob, 16), dtype=torch.float32).pin_memory()
             for _ in range(2)]
     done = [None, None]
-    depth = a.pipeline or (2 if n <= 96 else 1)
+    depth = a.pipeline or (2 if n <= 192 else 1)
     # --pipeline 2: step s runs on context / stream s % 2 (each context its
     # own records, poses and queue words), so consecutive steps are
     # independent and the GPU starts step s+1's kernels as step s's
     # persistent k_icp retires its workgroups
     ctxs = [youth_icp.IcpContext(W, H, max(n, 2), iters=a.iters, device=R.local)
             for _ in range(depth)]
+    # the steps in flight run side by side, each persistent k_icp on 1/depth
+    # of the workgroup slots (DESIGN.md §5 "Small shards")
+    share = depth if a.share == 0 else a.share
+    for c in ctxs:
+        c.set_concurrency(share)
     ctx = ctxs[0]
     streams = [main] + [torch.cuda.Stream() for _ in range(depth - 1)]
     it = [0]
@@ -401,10 +414,10 @@ def run_pairs(R):
         "global_pairs": n_glob, "pairs_per_gpu": n, "width": W, "height": H,
         "iters": a.iters, "fastdiv": ctx.fastdiv,
         "parallelism": f"dp{world} (contiguous pair shards, RCCL pose all-gather)",
-        "steps_in_flight": depth,
+        "steps_in_flight": depth, "k_icp_slot_share": f"1/{share}",
     }
     result["window_rates"] = [n_glob * a.steps / s for s in spread]
-    result["roofline"] = roofline_icp(a, kt, n, W, H)
+    result["roofline"] = roofline_icp(a, kt, n, W, H, share)
     result["roofline_prep"] = roofline_prep(a, kt, n, W, H)
     result["kernel_ms_per_step"] = {"k_icp": kt["k_icp"][0] / max(kt["k_icp"][1], 1),
                                     "k_prep": kt["k_prep"][0] / max(kt["prep_pass_steps"], 1)}

@@ -149,6 +149,19 @@ int youth_icp_fastdiv_enabled(youth_icp_ctx* ctx);
 int youth_icp_set_spec(youth_icp_ctx* ctx, int spec);
 int youth_icp_get_spec(const youth_icp_ctx* ctx);
 
+/* Concurrent batch aligns on one device (build-only; no SLAM.h counterpart).
+ * A caller that keeps `contexts` contexts' persistent aligns in flight at
+ * once on the same GPU (e.g. two steps of small batches on two streams)
+ * declares it on each of them: the persistent k_icp then runs on
+ * 1/contexts of the resident workgroup slots with 1/contexts of the work
+ * chunks, so the launches run side by side instead of each waiting for the
+ * other's slots (DESIGN.md §5 "Small shards").  Results are unchanged
+ * except in the last bits of the sums (their chunking differs).  1 (default)
+ * .. YOUTH_ICP_MAX_CONCURRENCY; returns the previous value, EINVAL
+ * otherwise.  The small-batch cooperative kernel is not affected. */
+#define YOUTH_ICP_MAX_CONCURRENCY 4
+int youth_icp_set_concurrency(youth_icp_ctx* ctx, int contexts);
+
 /* One-shot host API:  aligns n_pairs independent pairs; src and
  * dst are [n_pairs][H][W] int16 host arrays.  T_out: [n_pairs][16] row-major
  * fp32 4x4 with P_dst = T * P_src.  assoc_out: nullable [n_pairs][H*W] int32

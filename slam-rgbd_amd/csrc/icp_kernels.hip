@@ -2366,6 +2366,7 @@ struct youth_icp_ctx {
     int trk_batch = 1;                // frames per submission in youth_icp_track_host_sequence
     long long trk_chained = 0;        // micro-batch launches so far (youth_icp_track_chained)
     int queues = 0;                  // k_icp work queues (YOUTH_ICP_QUEUES=1..8; 0: by batch size)
+    int share = 1;                   // contexts launching k_icp concurrently (set_concurrency)
     int prep_xcd_map = 0;             // YOUTH_ICP_PREP_XCD_MAP=1: k_prep tiles contiguous per XCD (slower)
     // pipelined tracking (youth_icp_track_submit / _collect): up to
     // kTrackDepth frames in flight, each with a pinned staging buffer, pinned
@@ -2408,7 +2409,13 @@ static int reduce_geometry(const youth_icp_ctx* c, int n_pairs, int* chunk_out)
         const int v = e ? atoi(e) : 0;
         return v > 0 ? v : 0;
     }();
-    const int target_blocks = knob ? knob : (n_pairs <= 256 ? 2048 : 3072);
+    // a context that shares the device with share - 1 concurrent ones runs on
+    // 1/share of the workgroup slots, so it takes 1/share of the chunks: the
+    // same items per workgroup and iteration (youth_icp_set_concurrency).
+    // Shared, <= 96 pairs: 1536 / share (64 pairs, share 2: 768 chunks 81.6 K
+    // aligns/s, 1024 81.1 K, 1280 79.9 K; profiles/r03/ab_share.txt)
+    const int base = c->share > 1 && n_pairs <= 96 ? 1536 : (n_pairs <= 256 ? 2048 : 3072);
+    const int target_blocks = (knob ? knob : base) / c->share;
     int nb = (target_blocks + n_pairs - 1) / n_pairs;
     const int max_nb = (c->N + 2 * kRedStep - 1) / (2 * kRedStep);
     if (nb > max_nb) nb = max_nb;
@@ -2877,7 +2884,7 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
         const bool aligned = (reinterpret_cast<uintptr_t>(dsrc) % 8 == 0) && (c->W % 4 == 0);
         const int var = c->spec * 4 + (c->fast ? 2 : 0) + (aligned ? 1 : 0);
         const long long items = (long long)iters * n_pairs * nb;
-        long long grid = (long long)c->n_cu * c->icp_blocks_per_cu[var];
+        long long grid = (long long)c->n_cu * c->icp_blocks_per_cu[var] / c->share;
         if (grid > items) grid = items;
         if (grid < 1) grid = 1;
         const IterState is{c->d_T64,  c->d_T32,  c->d_status, c->d_stats,
@@ -3003,6 +3010,15 @@ int youth_icp_set_spec(youth_icp_ctx* c, int spec)
         return set_error(YOUTH_EINVAL, "set_spec: bad arguments (%d)", spec);
     const int old = c->spec;
     c->spec = spec;
+    return old;
+}
+
+int youth_icp_set_concurrency(youth_icp_ctx* c, int contexts)
+{
+    if (!c || contexts < 1 || contexts > YOUTH_ICP_MAX_CONCURRENCY)
+        return set_error(YOUTH_EINVAL, "set_concurrency: bad arguments (%d)", contexts);
+    const int old = c->share;
+    c->share = contexts;
     return old;
 }
 

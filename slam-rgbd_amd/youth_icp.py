@@ -86,6 +86,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "youth_icp_device_count": (c_int, []),
         "youth_icp_fastdiv_enabled": (c_int, [c_void_p]),
         "youth_icp_set_spec": (c_int, [c_void_p, c_int]),
+        "youth_icp_set_concurrency": (c_int, [c_void_p, c_int]),
         "youth_icp_get_spec": (c_int, [c_void_p]),
         "youth_icp_selftest_projquot": (c_int, [c_int, ctypes.c_longlong, ctypes.c_ulonglong,
                                                 POINTER(ctypes.c_longlong),
@@ -183,6 +184,7 @@ def _err(code: int) -> IcpError:
 
 TRACK_MAX_IN_FLIGHT = 16  # YOUTH_TRACK_MAX_IN_FLIGHT (include/youth_icp.h)
 TRACK_MAX_BATCH = 8       # YOUTH_TRACK_MAX_BATCH
+MAX_CONCURRENCY = 4       # YOUTH_ICP_MAX_CONCURRENCY
 
 
 def _check(code: int) -> int:
@@ -341,6 +343,12 @@ class IcpContext:
     def spec(self, value) -> None:
         code = {"fma": SPEC_FMA, "survey": SPEC_SURVEY}.get(value, value)
         _check(self._lib.youth_icp_set_spec(self._ctx, int(code)))
+
+    def set_concurrency(self, contexts: int) -> int:
+        """Declare `contexts` contexts aligning concurrently on this device
+        (youth_icp_set_concurrency): the persistent kernel takes 1/contexts of
+        the workgroup slots and chunks.  Returns the previous value."""
+        return _check(self._lib.youth_icp_set_concurrency(self._ctx, int(contexts)))
 
     def close(self):
         if getattr(self, "_ctx", None):

@@ -893,6 +893,62 @@ def test_headline_512_pairs_one_launch():
             assert np.array_equal(g_idx, oracle.associate(src[p], dst[p], T32[p][:3], K)), p
 
 
+def test_concurrent_contexts_share_the_device():
+    """youth_icp_set_concurrency(2) on two contexts whose persistent aligns
+    run side by side on two streams (bench.py's small shards, N = 8's 64
+    pairs): each k_icp on half the workgroup slots with half the chunks.
+    Both batches of 64 pairs @640x480, aligned twice in interleaved order,
+    within 1e-5 of the oracle with every pair's correspondence count at every
+    iteration equal to the oracle's, and the repeat bit-identical to the
+    first.  Out-of-range shares are refused and the setter returns the
+    previous value."""
+    import torch
+    n, W, H = 64, 640, 480
+    batches = [youth_synth.pairs(seed, n, W, H)[:2] for seed in (5, 6)]
+    dev = [(torch.from_numpy(s).cuda(), torch.from_numpy(d).cuda()) for s, d in batches]
+    outs = [torch.zeros((n, 16), dtype=torch.float32, device="cuda") for _ in range(2)]
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    torch.cuda.synchronize()
+    ctxs = [youth_icp.IcpContext(W, H, n, iters=10) for _ in range(2)]
+    try:
+        for c in ctxs:
+            with pytest.raises(youth_icp.IcpError):
+                c.set_concurrency(0)
+            with pytest.raises(youth_icp.IcpError):
+                c.set_concurrency(youth_icp.MAX_CONCURRENCY + 1)
+            assert c.set_concurrency(2) == 1
+        got = []
+        for rep in range(2):
+            for q in range(2):
+                ctxs[q].align_pairs_device(dev[q][0].data_ptr(), dev[q][1].data_ptr(), n,
+                                           d_T_out=outs[q].data_ptr(),
+                                           stream=streams[q].cuda_stream)
+            res = []
+            for q in range(2):
+                ctxs[q].sync(streams[q].cuda_stream)
+                assert ctxs[q].get_plan()["kernel"].startswith("k_prep + k_icp (persistent)")
+                T64, T32, st = ctxs[q].get_poses(n)
+                cnt, _ = ctxs[q].get_stats(n, 10)
+                assert np.array_equal(outs[q].cpu().numpy().reshape(n, 4, 4), T32)
+                res.append((T64, st, cnt))
+            got.append(res)
+        assert ctxs[0].set_concurrency(1) == 2
+    finally:
+        for c in ctxs:
+            c.close()
+    for q, (src, dst) in enumerate(batches):
+        T_cpu, st_cpu, stats = oracle.align_batch(src, dst, iters=10,
+                                                  n_threads=min(16, os.cpu_count() or 1),
+                                                  want_stats=True)
+        T64, st, cnt = got[0][q]
+        assert not st.any() and not st_cpu.any()
+        err = np.abs(T64[:, :3, :4] - T_cpu[:, :3, :4]).max()
+        assert float(err) <= POSE_TOL, (q, float(err))
+        assert np.array_equal(cnt, stats[..., 0]), (q, np.argwhere(cnt != stats[..., 0])[:4])
+        for a, b in zip(got[0][q], got[1][q]):
+            assert np.array_equal(a, b), q
+
+
 @pytest.mark.parametrize("xcd_map", ["1", "2"])
 def test_prep_tile_orders_bit_identical(xcd_map, monkeypatch):
     """k_prep's workgroup -> tile orders (YOUTH_ICP_PREP_XCD_MAP: 0 row-major
