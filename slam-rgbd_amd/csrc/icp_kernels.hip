@@ -1288,8 +1288,17 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
     int v0 = i / W;
     int u0 = i - v0 * W;
     int cnt = 0;
+    // kAligned: the next step's depth is loaded while this step's gathers
+    // and sums run (8 bytes per lane in flight), through a buffer descriptor
+    // over the frame, so the load past the last step returns 0 instead of
+    // faulting; its value is then never used
+    const __amdgpu_buffer_rsrc_t rdep = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<int16_t*>(sD), (short)0, W * H * (int)sizeof(int16_t), 0x00020000);
+    short4 dnext = kAligned && i < end ? __builtin_bit_cast(short4, __builtin_amdgcn_raw_buffer_load_b64(
+                                                                       rdep, i * 2, 0, 0))
+                                       : short4{};
     for (; i < end; i += kRedStep) {
-        const short4 d4 = load_depth4<kAligned>(sD, i, end);
+        const short4 d4 = kAligned ? dnext : load_depth4<kAligned>(sD, i, end);
         const int dd[4] = {d4.x, d4.y, d4.z, d4.w};
         float qx[4], qy[4], qz[4], fu[4], fv[4];
         LaneMask in[4];
@@ -1318,12 +1327,18 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
             u0 -= W;
             ++v0;
         }
-        // four 16-byte fetches back to back
+        // four 16-byte fetches back to back, then the next step's depth
         f4v t[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
             t[q] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rrec, (int)((unsigned)j[q] * 16u),
                                                                                  0, 0));
+        // (issued after the gathers: loads retire in order, so the match
+        // waits for gather q, vmcnt(4 - q), never wait for the depth)
+        asm volatile("" ::: "memory");
+        if (kAligned)
+            dnext = __builtin_bit_cast(
+                short4, __builtin_amdgcn_raw_buffer_load_b64(rdep, (i + kRedStep) * 2, 0, 0));
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const LaneMask okm = match_accumulate<kSp, kFast, true>(qx[q], qy[q], qz[q], t[q],
