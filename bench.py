@@ -73,8 +73,8 @@ def parse():
                          "streams, so step s+1's k_prep / k_icp fill step s's k_icp tail "
                          "(independent batches, each completed inside the timed region); "
                          "0 = auto: 2 for shards of <= 192 pairs, each k_icp on half the "
-                         "workgroup slots (--share; N = 8's 64 pairs: +4 %, N = 4's 128: "
-                         "+2 %), else 1 (256 pairs: neutral; profiles/r03/ab_share.txt)")
+                         "workgroup slots (--share; N = 8's 64 pairs: +4 %%, N = 4's 128: "
+                         "+2 %%), else 1 (256 pairs: neutral; profiles/r03/ab_share.txt)")
     ap.add_argument("--share", type=int, default=0, choices=[0, 1, 2, 3, 4],
                     help="pairs workload: k_icp slot share per context "
                          "(youth_icp_set_concurrency); 0 = the steps in flight")
@@ -241,6 +241,16 @@ def load_pmc(a, W, H):
     return tj, os.path.relpath(a.traffic_json, ROOT)
 
 
+# Same-box knockout timings of k_icp (profiles/r03/ab_knockout.txt): the share
+# of the kernel's time each instruction group accounts for when it is removed
+# (timing-only builds), next to the share the issue account prices it at.
+KNOCKOUTS = {
+    "source": "profiles/r03/ab_knockout.txt",
+    "fp64_update": {"measured_time_share": 0.16, "issue_account_share": 0.32},
+    "target_int_to_float": {"measured_time_share": 0.005, "issue_account_share": 0.033},
+}
+
+
 def roofline_icp(a, kt, n_pairs, W, H, concurrent=1):
     """Roofline of the dominant kernel, k_icp (persistent: all iterations of
     an align in ONE launch).  `achieved` = the kernel's algorithmic bytes
@@ -278,9 +288,14 @@ def roofline_icp(a, kt, n_pairs, W, H, concurrent=1):
         out["traffic_frac"] = traffic / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS
         out["traffic_over_algorithmic"] = traffic / alg
     if tj and "valu_busy_frac" in tj:
-        # what bounds k_icp: VALU issue, from the same PMC pass
-        out["limiter"] = "valu" if tj["valu_busy_frac"] > 0.8 else "hbm"
+        # what bounds k_icp: VALU issue plus the memory latency
+        # each wave exposes.  valu_issue_frac is the issue ACCOUNT of the same
+        # PMC pass (instruction counts x isolated per-form costs): an upper
+        # estimate that exceeds 1 when the mixed stream overlaps better than
+        # the isolated forms; the knockouts measure what is on the critical path
+        out["limiter"] = "valu issue + exposed latency" if tj["valu_busy_frac"] > 0.8 else "hbm"
         out["valu_issue_frac"] = tj["valu_busy_frac"]
+        out["critical_path"] = KNOCKOUTS
         out["valu"] = {k: tj[k] for k in ("valu_busy_frac", "valu_lane_ops_per_px_iteration",
                                           "valu_cycles_per_instruction", "effective_clock_ghz",
                                           "valu_busy_definition", "wave_state_frac",
