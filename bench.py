@@ -23,7 +23,8 @@ value: the C2 (one pair per call), C3 (1280x960, 20 iterations) and C5
 against the C oracle; the PCIe-inclusive host-buffer API; the viewer point
 list (§8 f4); and the CPU baseline (the C oracle on the host cores).
 
-Launch: python bench.py [--gpus 1] [--steps K] [--warmup W]
+Launch: python bench.py [--gpus N] [--steps K] [--warmup W]   (N > 1: bench.py starts
+        torch.distributed.run with N ranks as a child process and exits with its code)
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 Rank 0 prints ONE JSON line.
 """
@@ -34,6 +35,53 @@ import math
 import os
 import sys
 import time
+
+
+
+def _launch_ranks(argv=None, environ=None, run=None):
+    """`--gpus N` is the rank count (the driver's contract): without a
+    launcher (WORLD_SIZE unset) and N > 1, start N ranks through
+    torch.distributed.run as a CHILD process with the same arguments, let it
+    write to this process's stdout/stderr, and return its exit code.  Under a
+    launcher, --gpus must equal WORLD_SIZE (a mismatch would print a line whose
+    n_gpus is not the requested N).  Runs before torch is imported and before
+    any HIP call, so nothing here has touched the GPU.  Returns None when this
+    process is itself the (only) rank."""
+    import argparse as _ap
+    import socket
+    import subprocess
+    argv = sys.argv[1:] if argv is None else argv
+    environ = os.environ if environ is None else environ
+    p = _ap.ArgumentParser(add_help=False)
+    p.add_argument("--gpus", type=int, default=1)
+    n = p.parse_known_args(argv)[0].gpus
+    if n < 1:
+        sys.stderr.write(f"bench.py: --gpus {n} < 1\n")
+        return 2
+    ws = environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != n:
+            sys.stderr.write(f"bench.py: --gpus {n} != WORLD_SIZE {ws} under the launcher\n")
+            return 2
+        return None
+    if n == 1:
+        return None
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(n), "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + list(argv)
+    env = dict(environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")    # dmabuf IPC only on this pool
+    return (run or subprocess.call)(cmd, env=env)
+
+
+if __name__ == "__main__":
+    _rc = _launch_ranks()
+    if _rc is not None:
+        sys.exit(_rc)
 
 # torch first so libyouth_icp binds to torch's HIP runtime (DESIGN.md §6)
 import torch

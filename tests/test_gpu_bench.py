@@ -163,3 +163,19 @@ def test_bench_rccl_gather_one_gpu(workload):
     assert d["n_gpus"] == 1 and d["value"] > 0
     assert d["ranks"]["rccl_world_size"] == 1 and d["ranks"]["backend"] == "nccl"
     assert d["ranks"]["gather_timed"] and d["ranks"]["per_rank_ms"]["gather_ms"][0] > 0
+
+
+def test_bench_gpus_flag_self_launches_ranks():
+    """`python bench.py --gpus 2` with no launcher (the driver's form) starts
+    two ranks itself; gloo, so both fit on one GPU."""
+    env = dict(os.environ, YOUTH_BENCH_BACKEND="gloo")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup",
+                        "1", "--windows", "1", "--global-pairs", "64"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert d["ranks"]["rccl_world_size"] == 2 and d["ranks"]["backend"] == "gloo"
+    assert d["config"]["pairs_per_gpu"] == 32
