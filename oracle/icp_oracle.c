@@ -159,6 +159,66 @@ void oracle_associate(const float* sX, const float* sY, const float* sZ,
                            nZ, thr2, q);
 }
 
+static int g_reduce = ORACLE_REDUCE_EXACT;
+static oracle_lanes g_lanes = {ORACLE_LANES_STRIDED, 0, 0, 0};
+
+int oracle_set_reduce(int mode, const oracle_lanes* g)
+{
+    if (mode == ORACLE_REDUCE_EXACT) {
+        const int old = g_reduce;
+        g_reduce = mode;
+        return old;
+    }
+    if (mode != ORACLE_REDUCE_LANE32 || !g || g->threads < 64 || g->threads % 64 != 0)
+        return -1;
+    if (g->kind == ORACLE_LANES_STRIDED) {
+        if (g->chunk < 1) return -1;
+    } else if (g->kind == ORACLE_LANES_COOP || g->kind == ORACLE_LANES_COOP_TILE) {
+        if (g->npx < 1 || (g->kind == ORACLE_LANES_COOP_TILE && (g->npx * g->threads) % 64 != 0))
+            return -1;
+    } else {
+        return -1;
+    }
+    const int old = g_reduce;
+    g_reduce = mode;
+    g_lanes = *g;
+    return old;
+}
+
+int oracle_get_reduce(void) { return g_reduce; }
+
+/* Lane of source pixel i (u, v) under the partition g (icp_oracle.h), and
+ * the number of lanes of a W x H frame. */
+static long lane_of(const oracle_lanes* g, int W, int H, int i)
+{
+    const long T = g->threads;
+    if (g->kind == ORACLE_LANES_STRIDED) {
+        /* accumulate_chunk: i = start + 4 threadIdx + q + s (4 threads) */
+        const long c = i / g->chunk, o = i - c * g->chunk;
+        return c * T + (o % (4 * T)) / 4;
+    }
+    if (g->kind == ORACLE_LANES_COOP) {
+        /* k_icp_coop source staging: i = c npx T + s T + t */
+        const long C = (long)g->npx * T;
+        return (i / C) * T + (i % C) % T;
+    }
+    /* k_icp_coop tile_src: k = s T + t, u = x0 + k % 64, v = y0 + k / 64 */
+    const int th = (int)((long)g->npx * T / 64), tiles_x = (W + 63) / 64;
+    const int u = i % W, v = i / W, tx = u / 64, ty = v / th;
+    const long k = (long)(v - ty * th) * 64 + (u - tx * 64);
+    (void)H;
+    return ((long)ty * tiles_x + tx) * T + k % T;
+}
+
+static long lane_count(const oracle_lanes* g, int W, int H)
+{
+    const long N = (long)W * H, T = g->threads;
+    if (g->kind == ORACLE_LANES_STRIDED) return (N + g->chunk - 1) / g->chunk * T;
+    if (g->kind == ORACLE_LANES_COOP) return (N + (long)g->npx * T - 1) / ((long)g->npx * T) * T;
+    const int th = (int)((long)g->npx * T / 64);
+    return (long)((W + 63) / 64) * ((H + th - 1) / th) * T;
+}
+
 void oracle_reduce(const float* sX, const float* sY, const float* sZ,
                    const float* tX, const float* tY, const float* tZ,
                    const float* nX, const float* nY, const float* nZ,
@@ -169,6 +229,13 @@ void oracle_reduce(const float* sX, const float* sY, const float* sZ,
     const int N = W * H;
     double acc[ORACLE_NEQ];
     memset(acc, 0, sizeof(acc));
+    const int lanes32 = g_reduce == ORACLE_REDUCE_LANE32;
+    const long n_lanes = lanes32 ? lane_count(&g_lanes, W, H) : 0;
+    float* la = lanes32 ? (float*)calloc((size_t)n_lanes * 28, sizeof(float)) : NULL;
+    if (lanes32 && !la) {
+        for (int k = 0; k < ORACLE_NEQ; ++k) out[k] = NAN;
+        return;
+    }
     float q[3];
     for (int i = 0; i < N; ++i) {
         const int j = assoc_one(sX[i], sY[i], sZ[i], T, K, W, H, tX, tY, tZ, nX,
@@ -193,13 +260,29 @@ void oracle_reduce(const float* sX, const float* sY, const float* sZ,
         J[3] = nx;
         J[4] = ny;
         J[5] = nz;
+        acc[28] += 1.0;
+        if (lanes32) {
+            /* the kernels' match_accumulate with fp32 lanes: v_fma_f32 */
+            float* l = la + (size_t)lane_of(&g_lanes, W, H, i) * 28;
+            int k = 0;
+            for (int a = 0; a < 6; ++a)
+                for (int b = a; b < 6; ++b, ++k) l[k] = fmaf(J[a], J[b], l[k]);
+            for (int a = 0; a < 6; ++a) l[21 + a] = fmaf(J[a], r, l[21 + a]);
+            l[27] = fmaf(r, r, l[27]);
+            continue;
+        }
         int k = 0;
         for (int a = 0; a < 6; ++a)
             for (int b = a; b < 6; ++b)
                 acc[k++] += (double)J[a] * (double)J[b];
         for (int a = 0; a < 6; ++a) acc[21 + a] += (double)J[a] * (double)r;
         acc[27] += (double)r * (double)r;
-        acc[28] += 1.0;
+    }
+    if (lanes32) {
+        /* fp64 finalize: every lane's sums, converted, added in lane order */
+        for (long L = 0; L < n_lanes; ++L)
+            for (int k = 0; k < 28; ++k) acc[k] += (double)la[(size_t)L * 28 + k];
+        free(la);
     }
     memcpy(out, acc, sizeof(acc));
 }

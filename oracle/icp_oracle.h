@@ -57,6 +57,45 @@ typedef struct oracle_intrinsics {
 int oracle_set_spec(int spec);
 int oracle_get_spec(void);
 
+/* Reduction of spec a9 (the 28 sums of products and the count):
+ *   ORACLE_REDUCE_EXACT  every product of two fp32 values is exact in fp64;
+ *                        the products are summed in fp64 in pixel order;
+ *   ORACLE_REDUCE_LANE32 SURVEY.md §8a a9 as worded ("fp32 lanes -> fp64
+ *                        finalize"), the kernels' default: the source pixels
+ *                        are partitioned into lanes exactly as one kernel
+ *                        launch partitions them (oracle_lanes below); each
+ *                        lane sums its matched pixels' 28 products in fp32
+ *                        (fmaf, one rounding each, from +0, in increasing
+ *                        pixel order); every lane's 28 sums are then
+ *                        converted to fp64 and added in fp64.  The count is
+ *                        an integer in both modes.
+ * Lane partitions (each cites the kernel loop it restates):
+ *   ORACLE_LANES_STRIDED  k_icp / k_reduce (accumulate_chunk): workgroups of
+ *                        `threads` lanes own chunks of `chunk` pixels
+ *                        (chunk c = [c chunk, (c+1) chunk) of the frame); in
+ *                        every step of 4 threads pixels lane l takes pixels
+ *                        4l .. 4l+3;
+ *   ORACLE_LANES_COOP     k_icp_coop, contiguous chunks: workgroup c owns
+ *                        pixels [c npx threads, (c+1) npx threads), lane t of
+ *                        it the pixels c npx threads + s threads + t, s < npx;
+ *   ORACLE_LANES_COOP_TILE k_icp_coop with tile-shaped chunks: workgroup c
+ *                        owns target tile c (64 x tile_h pixels, tiles in
+ *                        raster order, tile_h = npx threads / 64), lane t the
+ *                        tile pixels k = s threads + t (k raster inside the
+ *                        tile: u = x0 + k % 64, v = y0 + k / 64).
+ * oracle_set_reduce returns the previous mode (-1: bad arguments; the
+ * geometry is ignored in EXACT mode and may be NULL there). */
+#define ORACLE_REDUCE_EXACT 0
+#define ORACLE_REDUCE_LANE32 1
+#define ORACLE_LANES_STRIDED 0
+#define ORACLE_LANES_COOP 1
+#define ORACLE_LANES_COOP_TILE 2
+typedef struct oracle_lanes {
+    int kind, chunk, threads, npx;
+} oracle_lanes; /* layout-identical to youth_lanes */
+int oracle_set_reduce(int mode, const oracle_lanes* geometry);
+int oracle_get_reduce(void);
+
 /* viewerModule.c:341-345 generalised.  Invalid pixel -> X=Y=Z=0. */
 void oracle_backproject(const int16_t* depth, int W, int H,
                         const oracle_intrinsics* K, float* X, float* Y, float* Z);
@@ -76,8 +115,8 @@ void oracle_associate(const float* sX, const float* sY, const float* sZ,
                       int W, int H, const oracle_intrinsics* K, const float T[12],
                       float dist_thresh, int32_t* idx);
 
-/* Point-to-plane normal equations (spec a8-a9) at pose T, accumulated in
- * fp64 in row-major pixel order.  out[29] as YOUTH_NEQ. */
+/* Point-to-plane normal equations (spec a8-a9) at pose T, summed as the
+ * reduction mode says (oracle_set_reduce).  out[29] as YOUTH_NEQ. */
 void oracle_reduce(const float* sX, const float* sY, const float* sZ,
                    const float* tX, const float* tY, const float* tZ,
                    const float* nX, const float* nY, const float* nZ,

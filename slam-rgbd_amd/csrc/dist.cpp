@@ -25,10 +25,9 @@ struct youth_dist {
     size_t staging_rows = 0;
     hipStream_t stream = nullptr;  // host variant's stream
     // every gather stages through `scratch`: calls are ordered across streams
-    // (the first call from a stream other than the previous call's waits for
-    // everything enqueued on that previous stream so far, its gather
-    // included), so double-buffering callers on two streams cannot mix
-    // batches in the scratch rows
+    // (`order` is recorded on a gather's stream right after it; a call from
+    // another stream waits on it), so double-buffering callers on two streams
+    // cannot mix batches in the scratch rows
     hipStream_t last = nullptr;
     bool any = false;
     hipEvent_t order = nullptr;
@@ -130,18 +129,14 @@ int youth_dist_allgather_poses(youth_dist* d, const float* d_local, int n_pairs,
     if (count > 0 && !d_local) return fail(YOUTH_EINVAL, "allgather_poses: null d_local");
     if (hipSetDevice(d->device) != hipSuccess) return fail(YOUTH_EHIP, "hipSetDevice");
     const hipStream_t s = (hipStream_t)stream;
-    if (d->any && d->last != s) {
-        // stream switch: mark the previous stream's work now and wait for it
-        // (a stream the caller destroyed since is rejected by the runtime:
-        // its work was released with it)
-        if (!d->order && hipEventCreateWithFlags(&d->order, hipEventDisableTiming) != hipSuccess)
-            return fail(YOUTH_EHIP, "hipEventCreate");
-        if (hipEventRecord(d->order, d->last) != hipSuccess) (void)hipGetLastError();
-        else if (hipStreamWaitEvent(s, d->order, 0) != hipSuccess)
-            return fail(YOUTH_EHIP, "hipStreamWaitEvent");
-    }
+    if (!d->order && hipEventCreateWithFlags(&d->order, hipEventDisableTiming) != hipSuccess)
+        return fail(YOUTH_EHIP, "hipEventCreate");
+    // stream switch: wait for the previous gather through the event recorded
+    // on ITS stream right after it (below); the previous stream's handle is
+    // never used again (the caller may have destroyed it)
+    if (d->any && d->last != s && hipStreamWaitEvent(s, d->order, 0) != hipSuccess)
+        return fail(YOUTH_EHIP, "hipStreamWaitEvent");
     d->last = s;
-    d->any = true;
     const size_t rows = (size_t)d->nranks * max_count;
     if (rows > d->scratch_rows) {
         // a previous gather may still read the old scratch on some stream
@@ -166,6 +161,8 @@ int youth_dist_allgather_poses(youth_dist* d, const float* d_local, int n_pairs,
     hipLaunchKernelGGL(k_compact, dim3((n_pairs * 4 + 255) / 256), dim3(256), 0, s,
                        (const float4*)d->scratch, max_count, n_pairs, d->nranks, (float4*)d_all);
     if (hipGetLastError() != hipSuccess) return fail(YOUTH_EHIP, "k_compact launch");
+    if (hipEventRecord(d->order, s) != hipSuccess) return fail(YOUTH_EHIP, "hipEventRecord");
+    d->any = true;
     return YOUTH_OK;
 }
 
@@ -223,9 +220,11 @@ void youth_dist_destroy(youth_dist* d)
 {
     if (!d) return;
     (void)hipSetDevice(d->device);
+    // the last gather (on whichever stream) completes before the
+    // communicator and the scratch it uses go away
     if (d->stream) (void)hipStreamSynchronize(d->stream);
+    if (d->any && d->order) (void)hipEventSynchronize(d->order);
     if (d->comm) (void)ncclCommDestroy(d->comm);
-    if (d->any && d->last) (void)hipStreamSynchronize(d->last);
     if (d->order) (void)hipEventDestroy(d->order);
     if (d->scratch) (void)hipFree(d->scratch);
     if (d->staging) (void)hipFree(d->staging);

@@ -2399,6 +2399,7 @@ struct youth_icp_ctx {
     int trk_dslot_last[2 * YOUTH_TRACK_MAX_BATCH];  // trk[] entry of the last launch that read depth slot d (-1: none)
     int trk_prev_d0 = -1;                       // first depth slot of the last launch
     int trk_head = 0, trk_n = 0;       // oldest in-flight submission, count in flight
+    int trk_cap = 2;                   // ring entries in use (grows to kTrackDepth on demand)
 
     // host-buffer batch API: H2D of chunk k+1 on xfer overlaps the align of chunk k
     hipStream_t xfer = nullptr;
@@ -2692,9 +2693,10 @@ struct PrepJob {
 //   * While every coop launch of the device has come from ONE stream, stream
 //     order is the total order: no extra packet.
 //   * The first launch from a second stream switches the device to ordered
-//     mode for good: it waits for an event recorded on the previous stream at
-//     that moment (everything enqueued there so far, the last coop grid
-//     included), and from then on every coop launch records the device's
+//     mode for good: the host waits once for the device to drain (the
+//     previous stream's last coop grid included; that stream's handle is not
+//     touched, the caller may have destroyed it), and from then on every
+//     coop launch records the device's
 //     completion event and waits on it when its stream differs from the
 //     previous launch's (an event record costs ~2.7 us per launch: 10.9 K).
 // YOUTH_ICP_COOP_LAUNCH=runtime restores hipLaunchCooperativeKernel.
@@ -2728,13 +2730,16 @@ static int coop_enqueue(youth_icp_ctx* c, hipStream_t s, void** args, int blocks
     if (o.any && o.last != s) {
         if (!o.done) HIP_TRY(hipEventCreateWithFlags(&o.done, hipEventDisableTiming));
         if (!o.multi) {
-            // first switch: mark the previous stream's work now (a stream the
-            // caller has destroyed since is rejected by the runtime: its work
-            // was released with it)
-            if (hipEventRecord(o.done, o.last) != hipSuccess) (void)hipGetLastError();
+            // first switch: the previous stream may be a caller's stream that
+            // has been destroyed since, so its handle is not used again
+            // (ADVICE r3); the host waits once for the device to drain, which
+            // covers that stream's last coop grid.  From now on every launch
+            // records `done` on its own stream right after it
+            HIP_TRY(hipDeviceSynchronize());
             o.multi = true;
+        } else {
+            HIP_TRY(hipStreamWaitEvent(s, o.done, 0));
         }
-        HIP_TRY(hipStreamWaitEvent(s, o.done, 0));
     }
     HIP_TRY(hipLaunchKernel(kern, grid, block, args, lds, s));
     if (o.multi) HIP_TRY(hipEventRecord(o.done, s));
@@ -3733,25 +3738,51 @@ int youth_icp_align_batch_multi(const int16_t* src, const int16_t* dst, int n_pa
 }
 
 // ------------------------------------------------------ frame tracking --
-// Lazily: the transfer stream, two pinned staging/result slots and events.
+// Lazily: the transfer stream and the ring's events.  The pinned staging
+// frame and result slot of a ring entry are allocated when a submission first
+// uses that entry (track_entry_pinned), so a context that keeps at most two
+// frames in flight (the SLAM worker) pins two frames, not the ring's 16
+// (16 x W x H x 2 bytes is 512 MB at 4096 x 4096).
 static int ensure_track(youth_icp_ctx* c)
 {
     if (c->trk[kTrackDepth - 1].done_nf) return YOUTH_OK;
     if (!c->xfer) HIP_TRY(hipStreamCreateWithFlags(&c->xfer, hipStreamNonBlocking));
     for (auto& q : c->trk) {
-        if (!q.pinned)
-            HIP_TRY(hipHostMalloc((void**)&q.pinned, (size_t)c->N * sizeof(int16_t),
-                                  hipHostMallocDefault));
-        if (!q.res)
-            HIP_TRY(hipHostMalloc((void**)&q.res, 17 * sizeof(double), hipHostMallocCoherent));
         if (!q.h2d) HIP_TRY(hipEventCreateWithFlags(&q.h2d, hipEventDisableTiming));
-    }
-    for (auto& q : c->trk) {
         if (!q.done) HIP_TRY(hipEventCreateWithFlags(&q.done, hipEventDisableTiming));
         if (!q.done_nf)
             HIP_TRY(hipEventCreateWithFlags(&q.done_nf,
                                             hipEventDisableTiming | hipEventDisableSystemFence));
     }
+    return YOUTH_OK;
+}
+
+// The ring holds trk_cap entries and grows only when a submission would put
+// more than trk_cap frames in flight: it is rotated so the oldest in-flight
+// entry is entry 0 (indices in trk_dslot_last follow), then extended, so the
+// in-flight entries stay consecutive modulo the new size.
+static void track_grow(youth_icp_ctx* c, int need)
+{
+    if (need <= c->trk_cap) return;
+    const int cap = c->trk_cap, h = c->trk_head;
+    if (h) {
+        youth_icp_ctx::TrackSlot tmp[kTrackDepth];
+        for (int i = 0; i < cap; ++i) tmp[i] = c->trk[(h + i) % cap];
+        for (int i = 0; i < cap; ++i) c->trk[i] = tmp[i];
+        for (int& d : c->trk_dslot_last)
+            if (d >= 0) d = (d - h + cap) % cap;
+        c->trk_head = 0;
+    }
+    c->trk_cap = std::min(kTrackDepth, need);
+}
+
+static int track_entry_pinned(youth_icp_ctx* c, int e)
+{
+    auto& q = c->trk[e];
+    if (!q.pinned)
+        HIP_TRY(hipHostMalloc((void**)&q.pinned, (size_t)c->N * sizeof(int16_t),
+                              hipHostMallocDefault));
+    if (!q.res) HIP_TRY(hipHostMalloc((void**)&q.res, 17 * sizeof(double), hipHostMallocCoherent));
     return YOUTH_OK;
 }
 
@@ -3807,7 +3838,12 @@ static int track_submit_frames(youth_icp_ctx* c, const int16_t* depth, int m,
     for (int r = 0, k = 0; r < nrs && k < m; ++r)
         if (r != ref) rs[k++] = r;
     int qi[kCoopMaxChain];
-    for (int i = 0; i < m; ++i) qi[i] = (c->trk_head + c->trk_n + i) % kTrackDepth;
+    track_grow(c, c->trk_n + m);
+    for (int i = 0; i < m; ++i) {
+        qi[i] = (c->trk_head + c->trk_n + i) % c->trk_cap;
+        const int rc = track_entry_pinned(c, qi[i]);  // before anything is enqueued
+        if (rc) return rc;
+    }
     auto& ql = c->trk[qi[m - 1]];
     // the caller's buffers are free on return: copy into the entries' pinned
     // staging, then H2D after the last launch that read these depth slots
@@ -3930,7 +3966,7 @@ int youth_icp_track_collect(youth_icp_ctx* c, double* T_rel, int* has_ref)
     int rc = bind_device(c);
     if (rc) return rc;
     auto& q = c->trk[c->trk_head];
-    c->trk_head = (c->trk_head + 1) % kTrackDepth;
+    c->trk_head = (c->trk_head + 1) % c->trk_cap;
     --c->trk_n;
     HIP_TRY(hipEventSynchronize(q.ev));
     if (has_ref) *has_ref = q.has_ref;

@@ -401,6 +401,42 @@ def test_sequence_c5_workload_640x480():
             assert np.array_equal(g_idx, oracle.associate(frames[k + 1], frames[k], T32[k][:3], K))
 
 
+def test_sequence_c5_full_length_one_call():
+    """Config C5 at its real length: the 1000-frame
+    640x480 sequence (seed 0x5EED1000) in ONE align_sequence_device call: 999
+    pairs, so the 3072-chunk work geometry and ~4.9 GB of target records (pair
+    880's frame lies past 2^32 bytes of records).  Reference anchor: the
+    serial frame-to-frame loop SLAM.cpp:32-63.  EVERY relative pose within
+    1e-5 of the oracle; per-iteration correspondence counts equal to the
+    oracle's on pairs 0/255/256/511/880/998; association indices at the final
+    fp32 pose bit-exact on pairs 0/880/998."""
+    import torch
+    F = 1000
+    frames, _ = youth_synth.sequence(0, F)
+    d = torch.from_numpy(frames).cuda()
+    torch.cuda.synchronize()
+    with youth_icp.IcpContext(640, 480, F - 1) as ctx:
+        ctx.align_sequence_device(d.data_ptr(), F)
+        ctx.sync()
+        T64, T32, st = ctx.get_poses(F - 1)
+        cnt, _ = ctx.get_stats(F - 1, 10)
+    del d
+    T_cpu, st_cpu = oracle.align_batch(frames[1:], frames[:-1], iters=10,
+                                       n_threads=min(16, os.cpu_count() or 1))
+    assert np.array_equal(st, st_cpu) and not st.any()
+    err = [_pose_err(T64[k], T_cpu[k]) for k in range(F - 1)]
+    assert max(err) <= POSE_TOL, (int(np.argmax(err)), max(err))
+    K = oracle.viewer_K(640, 480)
+    with youth_icp.IcpContext(640, 480, 2) as one:
+        for k in (0, 255, 256, 511, 880, 998):
+            _, _, _, stats = oracle.align(frames[k + 1], frames[k], iters=10)
+            assert np.array_equal(cnt[k], stats[:, 0]), k
+            if k in (0, 880, 998):
+                g_idx, _ = one.reduce(frames[k + 1], frames[k], T32[k][:3])
+                assert np.array_equal(
+                    g_idx, oracle.associate(frames[k + 1], frames[k], T32[k][:3], K)), k
+
+
 def test_track_frame_matches_oracle():
     frames, _ = youth_synth.sequence(0, 5)
     with youth_icp.IcpContext(640, 480, 2) as ctx:
