@@ -150,6 +150,11 @@ def parse():
                     help="arithmetic of spec a7/a8 (youth_icp_set_spec): survey = SURVEY.md §8a "
                          "as worded (the default), fma = the opt-in fma-chain form; the oracle "
                          "checks in the same spec")
+    ap.add_argument("--reduce", choices=["lane32", "exact"],
+                    default=os.environ.get("YOUTH_ICP_REDUCE", "lane32"),
+                    help="spec a9's reduction (youth_icp_set_reduce): lane32 = SURVEY.md §8a a9 as "
+                         "worded, fp32 lane sums -> fp64 finalize (the default); exact = every "
+                         "product exact in fp64 (opt-in)")
     ap.add_argument("--no-spec-parity", action="store_true",
                     help="skip the spec-parity leg (rank 0, N=1)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -516,6 +521,7 @@ def run_pairs(R):
         if not a.no_spec_parity:
             leg["spec_parity"] = spec_parity(a, main)
             leg["spec_parity"]["other_spec_rate"] = other_spec_rate(R, ctxs, step, n_glob)
+            leg["spec_parity"]["other_reduce_rate"] = other_reduce_rate(R, ctxs, step, n_glob)
         result.update(leg)
     for c in ctxs:
         c.close()
@@ -566,13 +572,36 @@ def other_spec_rate(R, ctxs, step, n_glob):
             "k_icp_ms": ms / max(n, 1)}
 
 
+def other_reduce_rate(R, ctxs, step, n_glob):
+    """The headline step with the OTHER spec a9 reduction (lane32 <-> exact)
+    on the same contexts and inputs (after the timed region)."""
+    a = R.a
+    other = "exact" if a.reduce == "lane32" else "lane32"
+    torch.cuda.synchronize()
+    for c in ctxs:
+        c.reduction = other
+    for _ in range(5):
+        step()
+    g = CtxGroup(ctxs)
+    g.set_timing(True, iteration_kernel_only=True)
+    el = R.window(step, a.steps)
+    ms, n = g.get_timing(0)
+    g.set_timing(False)
+    for c in ctxs:
+        c.reduction = a.reduce
+    return {"reduce": other, "value": n_glob * a.steps / el, "unit": "aligns/s",
+            "k_icp_ms": ms / max(n, 1)}
+
+
 def spec_parity(a, main):
-    """how far the GPU's poses sit from SURVEY §8a's
-    literal arithmetic (the survey-spec oracle) in each spec the kernels
-    implement, on C2's 640x480 pairs (64), C3 (2 pairs at 1280x960, 20
-    iterations), C5 (a 201-frame sequence: 200 relative poses) and at SURVEY
-    §8d's noise (16 pairs).  Also each spec against the oracle in the same
-    spec (the bit-exactness bar, ~1e-13)."""
+    """how far the GPU's poses sit from the
+    survey-spec oracle with exact products (SURVEY §8a a7/a8 as worded, the
+    strictest sums) in each arithmetic x reduction the kernels implement, on
+    C2's 640x480 pairs (64), C3 (2 pairs at 1280x960, 20 iterations), C5 (a
+    201-frame sequence: 200 relative poses) and at SURVEY §8d's noise (16
+    pairs).  Also each variant against the oracle run in the same variant
+    (lane32: the oracle's lane sums over the GPU launch's own lane partition,
+    youth_icp_get_lanes): the bit-exactness bar, ~1e-13."""
     oracle = oracle_mod()
     cases = {}
     s64 = youth_synth.pairs(0, 64)
@@ -584,36 +613,51 @@ def spec_parity(a, main):
     sn = youth_synth.pairs(0, 16, flags=youth_synth.SURVEY_FLAGS)
     cases["survey_noise_16_pairs"] = (sn[0], sn[1], 640, 480, 10, None)
     out = {}
-    worst = {}
+    worst, same = {}, {}
     for name, (src, dst, W, H, iters, frames) in cases.items():
         n = src.shape[0]
         K = youth_icp.default_intrinsics(W, H)
         row = {"pairs": n}
         ref = {}
+
+        def oracle_poses(sp, lanes):
+            with oracle.spec(sp), oracle.reduction("lane32" if lanes else "exact", lanes):
+                return oracle.align_batch(src, dst, K=oracle.viewer_K(W, H), iters=iters,
+                                          n_threads=min(n, _cpus()))[0]
+
         for sp in ("survey", "fma"):
-            with oracle.spec(sp):
-                ref[sp], _ = oracle.align_batch(src, dst, K=oracle.viewer_K(W, H), iters=iters,
-                                                n_threads=min(n, _cpus()))
+            ref[sp, "exact"] = oracle_poses(sp, None)
         ctx = youth_icp.IcpContext(W, H, max(n, 2), K=K, iters=iters)
         if frames is not None:
             df = torch.from_numpy(frames).cuda()
         else:
             ds, dd = torch.from_numpy(src).cuda(), torch.from_numpy(dst).cuda()
         for sp in ("survey", "fma"):
-            ctx.spec = sp
-            if frames is not None:
-                ctx.align_sequence_device(df.data_ptr(), n + 1, stream=main.cuda_stream)
-            else:
-                ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), n, stream=main.cuda_stream)
-            T, _, st = ctx.get_poses(n)
-            row[f"gpu_{sp}_vs_survey_oracle"] = pose_err(T, ref["survey"])
-            row[f"gpu_{sp}_vs_{sp}_oracle"] = pose_err(T, ref[sp])
-            row[f"gpu_{sp}_status_nonzero"] = int((st != 0).sum())
-            worst[sp] = max(worst.get(sp, 0.0), row[f"gpu_{sp}_vs_survey_oracle"])
+            for red in ("lane32", "exact"):
+                ctx.spec, ctx.reduction = sp, red
+                if frames is not None:
+                    ctx.align_sequence_device(df.data_ptr(), n + 1, stream=main.cuda_stream)
+                else:
+                    ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), n,
+                                           stream=main.cuda_stream)
+                T, _, st = ctx.get_poses(n)
+                if red == "lane32":
+                    lanes = ctx.lanes()
+                    row["lanes"] = dict(zip(("kind", "chunk", "threads", "npx"), lanes))
+                    ref[sp, red] = oracle_poses(sp, lanes)
+                v = sp if red == "exact" else f"{sp}_{red}"
+                row[f"gpu_{v}_vs_survey_oracle"] = pose_err(T, ref["survey", "exact"])
+                row[f"gpu_{v}_vs_same_variant_oracle"] = pose_err(T, ref[sp, red])
+                row[f"gpu_{v}_status_nonzero"] = int((st != 0).sum())
+                worst[v] = max(worst.get(v, 0.0), row[f"gpu_{v}_vs_survey_oracle"])
+                same[v] = max(same.get(v, 0.0), row[f"gpu_{v}_vs_same_variant_oracle"])
         ctx.close()
         out[name] = row
     out["max_vs_survey_oracle"] = worst
-    out["default_within_tol_of_survey_spec"] = bool(worst[a.spec] <= POSE_TOL)
+    out["max_vs_same_variant_oracle"] = same
+    dv = a.spec if a.reduce == "exact" else f"{a.spec}_{a.reduce}"
+    out["default_variant"] = dv
+    out["default_within_tol_of_survey_spec"] = bool(worst[dv] <= POSE_TOL)
     return out
 
 
@@ -1001,7 +1045,11 @@ def base_result(R, value, elapsed):
         "spec": {"name": a.spec,
                  "a7_a8": ("SURVEY.md §8a as worded: no FMA, IEEE division fx P'x / P'z"
                            if a.spec == "survey" else
-                           "fma chains, one correctly rounded reciprocal (opt-in)")},
+                           "fma chains, one correctly rounded reciprocal (opt-in)"),
+                 "a9_reduce": a.reduce,
+                 "a9": ("SURVEY.md §8a a9 as worded: fp32 lane sums (one fma each), fp64 finalize"
+                        if a.reduce == "lane32" else
+                        "every product exact in fp64 (opt-in)")},
         "data": "synthetic (ray-cast room scene, int16 mm depth, seeds 0x5EED0000+pair / "
                 "0x5EED1000 sequence)",
     }
@@ -1087,6 +1135,7 @@ def cpu_baseline(a, src, dst, T_gpu):
 def main():
     a = parse()
     os.environ["YOUTH_ICP_SPEC"] = a.spec   # every context of this run (youth_icp_create)
+    os.environ["YOUTH_ICP_REDUCE"] = a.reduce
     R = Run(a)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))   # the checker (legs after timing)
     # a non-default torch stream: its handle is what every align is issued on,

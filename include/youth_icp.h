@@ -149,6 +149,39 @@ int youth_icp_fastdiv_enabled(youth_icp_ctx* ctx);
 int youth_icp_set_spec(youth_icp_ctx* ctx, int spec);
 int youth_icp_get_spec(const youth_icp_ctx* ctx);
 
+/* Reduction of spec a9 (the 28 sums of J J^T, J r, r^2):
+ *   YOUTH_REDUCE_LANE32 (default) SURVEY.md §8a a9 as worded, "fp32 lanes ->
+ *                     fp64 finalize": each GPU lane sums its matched pixels'
+ *                     28 products with one fp32 fma each over its whole share
+ *                     of an iteration, converts them to fp64 once, and the
+ *                     lanes are added in fp64 (fixed order);
+ *   YOUTH_REDUCE_EXACT opt-in: every product of two fp32 values exact in fp64
+ *                     (one fp64 fma per product), ~10 % slower k_icp.
+ * youth_icp_set_reduce returns the previous mode (EINVAL for another value);
+ * the environment YOUTH_ICP_REDUCE=lane32|exact sets a new context's initial
+ * mode.  youth_icp_get_lanes reports how the last align partitioned each
+ * iteration's source pixels into lanes (the oracle's oracle_set_reduce
+ * restates a LANE32 iteration exactly given that partition):
+ *   YOUTH_LANES_STRIDED   workgroups of `threads` lanes own chunks of `chunk`
+ *                         pixels; in each step of 4 threads pixels, lane l
+ *                         takes pixels 4l .. 4l+3 (k_icp, k_reduce);
+ *   YOUTH_LANES_COOP      workgroup c owns [c npx threads, (c+1) npx threads),
+ *                         lane t the pixels c npx threads + s threads + t;
+ *   YOUTH_LANES_COOP_TILE workgroup c owns target tile c (64 x npx threads/64
+ *                         pixels, raster order), lane t the tile pixels
+ *                         k = s threads + t. */
+#define YOUTH_REDUCE_EXACT  0
+#define YOUTH_REDUCE_LANE32 1
+#define YOUTH_LANES_STRIDED   0
+#define YOUTH_LANES_COOP      1
+#define YOUTH_LANES_COOP_TILE 2
+typedef struct youth_lanes {
+    int kind, chunk, threads, npx;
+} youth_lanes;
+int youth_icp_set_reduce(youth_icp_ctx* ctx, int mode);
+int youth_icp_get_reduce(const youth_icp_ctx* ctx);
+int youth_icp_get_lanes(const youth_icp_ctx* ctx, youth_lanes* out);
+
 /* Concurrent batch aligns on one device (build-only; no SLAM.h counterpart).
  * A caller that keeps `contexts` contexts' persistent aligns in flight at
  * once on the same GPU (e.g. two steps of small batches on two streams)

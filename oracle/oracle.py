@@ -55,6 +55,9 @@ def load_library() -> ctypes.CDLL:
     lib.oracle_set_spec.argtypes = [c_int]
     lib.oracle_set_spec.restype = c_int
     lib.oracle_get_spec.restype = c_int
+    lib.oracle_set_reduce.argtypes = [c_int, ctypes.c_void_p]
+    lib.oracle_set_reduce.restype = c_int
+    lib.oracle_get_reduce.restype = c_int
     lib.oracle_max_threads.restype = c_int
     lib.oracle_viewer_cloud.argtypes = [P16, POINTER(ctypes.c_uint8), c_int, c_int, PK, PF]
     lib.oracle_viewer_cloud.restype = c_int
@@ -98,6 +101,56 @@ class spec:
 
     def __exit__(self, *exc):
         set_spec(self.old)
+
+
+REDUCE_EXACT = 0   # ORACLE_REDUCE_EXACT: exact fp64 products, pixel order
+REDUCE_LANE32 = 1  # ORACLE_REDUCE_LANE32: fp32 lanes -> fp64 finalize
+REDUCES = {"exact": REDUCE_EXACT, "lane32": REDUCE_LANE32}
+LANES_STRIDED, LANES_COOP, LANES_COOP_TILE = 0, 1, 2
+
+
+class OracleLanes(ctypes.Structure):
+    _fields_ = [("kind", c_int), ("chunk", c_int), ("threads", c_int), ("npx", c_int)]
+
+
+def set_reduce(mode, lanes=None) -> int:
+    """Select spec a9's reduction ("exact" | "lane32" or 0 | 1).  LANE32 needs
+    the lane partition of the kernel launch it restates: a (kind, chunk,
+    threads, npx) tuple, e.g. youth_icp.Context.lanes().  Returns the
+    previous mode."""
+    global _lanes
+    code = REDUCES.get(mode, mode)
+    g = None if lanes is None else OracleLanes(*[int(v) for v in lanes])
+    lib = load_library()
+    old = lib.oracle_set_reduce(int(code), None if g is None else ctypes.byref(g))
+    if old < 0:
+        raise ValueError(f"bad reduce mode {mode!r} / lanes {lanes!r}")
+    if int(code) == REDUCE_LANE32:
+        _lanes = tuple(int(v) for v in lanes)
+    return old
+
+
+_lanes = None   # the geometry of the last LANE32 selection
+
+
+def get_reduce() -> int:
+    return load_library().oracle_get_reduce()
+
+
+class reduction:
+    """Context manager: ``with oracle.reduction("lane32", lanes): ...``;
+    restores the previous mode (and geometry) on exit."""
+
+    def __init__(self, mode, lanes=None):
+        self.mode, self.lanes = mode, lanes
+
+    def __enter__(self):
+        self.prev_lanes = _lanes
+        self.old = set_reduce(self.mode, self.lanes)
+        return self
+
+    def __exit__(self, *exc):
+        set_reduce(self.old, self.prev_lanes if self.old == REDUCE_LANE32 else None)
 
 
 def K_of(K) -> OracleIntrinsics:

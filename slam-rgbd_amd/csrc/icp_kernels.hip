@@ -37,6 +37,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -178,6 +179,17 @@ __device__ __forceinline__ float proj_rcp_rn(float den)
 // (k_icp, k_icp_coop, k_reduce) is instantiated for each.
 constexpr int kSpecFma = YOUTH_SPEC_FMA;
 constexpr int kSpecSurvey = YOUTH_SPEC_SURVEY;
+// ... and for each reduction of spec a9 (youth_icp_set_reduce):
+//   lane32 (default) SURVEY.md §8a a9 as worded, "fp32 lanes -> fp64
+//          finalize": each lane sums its pixels' 28 products with v_fma_f32
+//          over its whole share of a work item, then converts once;
+//   exact  every product exact in fp64 (v_fmac_f64 per product).
+// The kernels' template parameter kSp is the VARIANT: bit 0 the arithmetic
+// (kSpecFma / kSpecSurvey), bit 1 (kRedLane32) the lane32 reduction.
+constexpr int kRedLane32 = 2;
+constexpr int kVariants = 4;
+__host__ __device__ constexpr bool sp_survey(int v) { return (v & 1) == kSpecSurvey; }
+__host__ __device__ constexpr bool sp_lane32(int v) { return (v & kRedLane32) != 0; }
 
 // kSpecSurvey's projection quotient RN(n / den) from r = RN(1 / den)
 // (proj_recip inside proj_den_ok: correctly rounded, checked exhaustively):
@@ -1133,7 +1145,7 @@ __device__ __forceinline__ void xform_project(const float* T, float sx, float sy
                                               const Intr& K, int W, int H, float& qx, float& qy,
                                               float& qz, float& fu, float& fv, LaneMask& inm, int& j)
 {
-    if (kSp == kSpecSurvey) {
+    if (sp_survey(kSp)) {
         qx = ((T[0] * sx + T[1] * sy) + T[2] * sz) + T[3];
         qy = ((T[4] * sx + T[5] * sy) + T[6] * sz) + T[7];
         qz = ((T[8] * sx + T[9] * sy) + T[10] * sz) + T[11];
@@ -1204,22 +1216,24 @@ __device__ __forceinline__ void xform_project(const float* T, float sx, float sy
 //       d2 = fma(dz, dz, fma(dy, dy, dx dx));
 //   a8  r = n.(P' - P_t) = fma(n2, dz, fma(n1, dy, n0 dx));
 //       J = [P' x n, n], (P' x n)_0 = fma(qy, n2, -(qz n1)) etc.;
-//   a9  the 28 products of fp32 values are exact in fp64; one rounding per
-//       add.  Unmatched lanes skip the update, or add J = 0 and r = +-0,
-//       which leaves every sum unchanged.  The target's x, y are recomputed from its z with
+//   a9  lane32 (A = float): acc = fma(J_a, J_b, acc) in fp32, one rounding
+//       per product-add; exact (A = double): the 28 products of fp32 values
+//       are exact in fp64, one rounding per add.  Unmatched lanes skip the
+//       update, or add J = 0 and r = +-0, which leaves every sum unchanged
+//       (an accumulator is never -0: it starts at +0 and x + -x is +0).  The target's x, y are recomputed from its z with
 //       k_prep's expression (bit-identical to the stored plane).
 //   kSpecSurvey: d2 = (dx dx + dy dy) + dz dz, r = (n0 dx + n1 dy) + n2 dz,
 //       (P' x n)_0 = qy n2 - qz n1 etc. (no FMA).
-template <int kSp, bool kFast, bool kSkip>
+template <int kSp, bool kFast, bool kSkip, typename A>
 __device__ __forceinline__ LaneMask match_accumulate(float qx, float qy, float qz, f4v t, float fu,
                                                      float fv, LaneMask inm, const Intr& K,
-                                                     const FastK& F, float thr2, double* acc)
+                                                     const FastK& F, float thr2, A* acc)
 {
     const float tz = t.x;
     const float tx = bp_div<kFast>((fu - K.cx) * tz, K.fx, F.hfx, F.lfx);
     const float ty = bp_div<kFast>((fv - K.cy) * tz, K.fy, F.hfy, F.lfy);
     const float dx = qx - tx, dy = qy - ty, dz = qz - tz;
-    const float d2 = kSp == kSpecSurvey ? (dx * dx + dy * dy) + dz * dz
+    const float d2 = sp_survey(kSp) ? (dx * dx + dy * dy) + dz * dz
                                         : fmaf(dz, dz, fmaf(dy, dy, dx * dx));
     const LaneMask okm = inm & mask_gt(tz, 0.0f) & mask_lt(d2, thr2);
     // kSkip (the throughput kernels): unmatched lanes leave the sums
@@ -1234,7 +1248,7 @@ __device__ __forceinline__ LaneMask match_accumulate(float qx, float qy, float q
         const float n1 = kSkip || ok ? t.z : 0.0f;
         const float n2 = kSkip || ok ? t.w : 0.0f;
         float r, Jf[6];
-        if (kSp == kSpecSurvey) {
+        if (sp_survey(kSp)) {
             r = (n0 * dx + n1 * dy) + n2 * dz;
             Jf[0] = qy * n2 - qz * n1;
             Jf[1] = qz * n0 - qx * n2;
@@ -1249,16 +1263,29 @@ __device__ __forceinline__ LaneMask match_accumulate(float qx, float qy, float q
         Jf[4] = n1;
         Jf[5] = n2;
         int k = 0;
+        if constexpr (sizeof(A) == sizeof(float)) {
 #pragma unroll
-        for (int a = 0; a < 6; ++a)
+            for (int a = 0; a < 6; ++a)
 #pragma unroll
-            for (int bb = a; bb < 6; ++bb) {
-                acc[k] = fma((double)Jf[a], (double)Jf[bb], acc[k]);
-                ++k;
-            }
+                for (int bb = a; bb < 6; ++bb) {
+                    acc[k] = fmaf(Jf[a], Jf[bb], acc[k]);
+                    ++k;
+                }
 #pragma unroll
-        for (int a = 0; a < 6; ++a) acc[21 + a] = fma((double)Jf[a], (double)r, acc[21 + a]);
-        acc[27] = fma((double)r, (double)r, acc[27]);
+            for (int a = 0; a < 6; ++a) acc[21 + a] = fmaf(Jf[a], r, acc[21 + a]);
+            acc[27] = fmaf(r, r, acc[27]);
+        } else {
+#pragma unroll
+            for (int a = 0; a < 6; ++a)
+#pragma unroll
+                for (int bb = a; bb < 6; ++bb) {
+                    acc[k] = fma((double)Jf[a], (double)Jf[bb], acc[k]);
+                    ++k;
+                }
+#pragma unroll
+            for (int a = 0; a < 6; ++a) acc[21 + a] = fma((double)Jf[a], (double)r, acc[21 + a]);
+            acc[27] = fma((double)r, (double)r, acc[27]);
+        }
     }
     return okm;
 }
@@ -1288,6 +1315,11 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
     int v0 = i / W;
     int u0 = i - v0 * W;
     int cnt = 0;
+    // lane32: this lane's fp32 sums over its whole share of the chunk,
+    // converted to fp64 once at the end (acc enters zeroed)
+    float facc[28];
+#pragma unroll
+    for (int q = 0; q < 28; ++q) facc[q] = 0.0f;
     // kAligned: the next step's depth is loaded while this step's gathers
     // and sums run (8 bytes per lane in flight), through a buffer descriptor
     // over the frame, so the load past the last step returns 0 instead of
@@ -1341,14 +1373,22 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
                 short4, __builtin_amdgcn_raw_buffer_load_b64(rdep, (i + kRedStep) * 2, 0, 0));
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const LaneMask okm = match_accumulate<kSp, kFast, true>(qx[q], qy[q], qz[q], t[q],
-                                                                    fu[q], fv[q], in[q], K, F,
-                                                                    thr2, acc);
+            LaneMask okm;
+            if constexpr (sp_lane32(kSp))
+                okm = match_accumulate<kSp, kFast, true>(qx[q], qy[q], qz[q], t[q], fu[q], fv[q],
+                                                         in[q], K, F, thr2, facc);
+            else
+                okm = match_accumulate<kSp, kFast, true>(qx[q], qy[q], qz[q], t[q], fu[q], fv[q],
+                                                         in[q], K, F, thr2, acc);
             if (kAssoc && (i + q) < end) arow[i + q] = lane_in(okm) ? j[q] : -1;
             // matches counted per wave on the scalar unit (s_bcnt1 of the
             // match mask) instead of a per-lane select and add
             cnt += __builtin_popcountll(okm);
         }
+    }
+    if constexpr (sp_lane32(kSp)) {
+#pragma unroll
+        for (int q = 0; q < 28; ++q) acc[q] = (double)facc[q];
     }
     // the wave's count, carried by lane 0 into the wave / workgroup sums
     acc[28] += (threadIdx.x & 63) == 0 ? (double)cnt : 0.0;
@@ -1974,12 +2014,12 @@ __device__ unsigned long long* coop_phase;
 // s0 .. s0+Q-1 of this lane in the LDS planes X/Y/Z [slot][256]): transform,
 // project, Q record gathers back to back, residual, Jacobian, exact products
 // into the fp64 accumulators.  Same expressions as accumulate_chunk.
-template <int kSp, bool kFast, int Q, int kThreads>
+template <int kSp, bool kFast, int Q, int kThreads, typename A>
 __device__ __forceinline__ void coop_group(const float* __restrict__ X, const float* __restrict__ Y,
                                            const float* __restrict__ Z, int s0, const float* T,
                                            __amdgpu_buffer_rsrc_t rrec, int W, int H,
                                            const Intr& K, const FastK& F, float thr2,
-                                           double* acc, int& nmatch)
+                                           A* acc, int& nmatch)
 {
     const int t = threadIdx.x;
     float qx[Q], qy[Q], qz[Q], fu[Q], fv[Q];
@@ -2160,18 +2200,23 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
         for (int q = 0; q < 12; ++q)
             T[q] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sh_T[q])));
         double acc[kNeq];
+        // lane32: the lane's fp32 sums over its npx pixels, converted once
+        typedef std::conditional_t<sp_lane32(kSp), float, double> A;
+        A la[28];
 #pragma unroll
-        for (int q = 0; q < kNeq; ++q) acc[q] = 0.0;
+        for (int q = 0; q < 28; ++q) la[q] = A(0);
         int nmatch = 0;
         int s0 = 0;
         for (; s0 + 4 <= npx; s0 += 4)
-            coop_group<kSp, kFast, 4, kThreads>(X, Y, Z, s0, T, rrec, W, H, K, F, thr2, acc, nmatch);
+            coop_group<kSp, kFast, 4, kThreads>(X, Y, Z, s0, T, rrec, W, H, K, F, thr2, la, nmatch);
         switch (npx - s0) {  // wave-uniform tail
-        case 3: coop_group<kSp, kFast, 3, kThreads>(X, Y, Z, s0, T, rrec, W, H, K, F, thr2, acc, nmatch); break;
-        case 2: coop_group<kSp, kFast, 2, kThreads>(X, Y, Z, s0, T, rrec, W, H, K, F, thr2, acc, nmatch); break;
-        case 1: coop_group<kSp, kFast, 1, kThreads>(X, Y, Z, s0, T, rrec, W, H, K, F, thr2, acc, nmatch); break;
+        case 3: coop_group<kSp, kFast, 3, kThreads>(X, Y, Z, s0, T, rrec, W, H, K, F, thr2, la, nmatch); break;
+        case 2: coop_group<kSp, kFast, 2, kThreads>(X, Y, Z, s0, T, rrec, W, H, K, F, thr2, la, nmatch); break;
+        case 1: coop_group<kSp, kFast, 1, kThreads>(X, Y, Z, s0, T, rrec, W, H, K, F, thr2, la, nmatch); break;
         default: break;
         }
+#pragma unroll
+        for (int q = 0; q < 28; ++q) acc[q] = (double)la[q];
         acc[28] = lane == 0 ? (double)nmatch : 0.0;  // the wave's count, lane 0
         COOP_MARK(k, 1);
         if (wave < 4) COOP_MARK_WAVE(k, 11 + wave);  // slots 12-14: waves 1-3 pixel loop done
@@ -2352,7 +2397,10 @@ struct youth_icp_ctx {
     unsigned* d_epoch = nullptr;     // [max_frames] persistent pose epochs
     unsigned* d_head = nullptr;      // queue words kQHead / kQError / kQSpins / kQWaited
     bool persistent = true;          // one k_icp launch per align (else per-iteration k_reduce)
-    int icp_blocks_per_cu[8] = {};  // occupancy of k_icp<spec, fast, aligned> [spec 4 + fast 2 + aligned]
+    int reduce = YOUTH_REDUCE_LANE32; // spec a9 (youth_icp_set_reduce, YOUTH_ICP_REDUCE)
+    youth_lanes lanes{};             // lane partition of the last align's iterations
+    bool has_lanes = false;
+    int icp_blocks_per_cu[4 * kVariants] = {};  // occupancy of k_icp<variant, fast, aligned> [variant 4 + fast 2 + aligned]
     int n_cu = 0;
     // small batches: k_icp_coop (youth_icp_create reads the knobs)
     bool coop = true;                // YOUTH_ICP_NO_COOP=1 disables
@@ -2362,9 +2410,9 @@ struct youth_icp_ctx {
     int coop_max_pairs = kCoopMaxPairs;  // YOUTH_ICP_COOP_MAX_PAIRS (<= kCoopMaxPairs)
     int coop_launch = 0;             // YOUTH_ICP_COOP_LAUNCH: 0 serial (default), 1 runtime, 2 plain
     bool coop_refuse = false;        // YOUTH_ICP_TEST_REFUSE_COOP=1 (test hook)
-    // occupancy of k_icp_coop<spec, fast, threads> [threads 256?][spec 2 + fast] at npx (LDS)
-    int coop_bpc[2][4][kCoopMaxPx + 1] = {};
-    int coop_bpc_tall[4] = {};              // the 64 x 80 prep-tile kernel at 10 px per lane
+    // occupancy of k_icp_coop<variant, fast, threads> [threads 256?][variant 2 + fast] at npx (LDS)
+    int coop_bpc[2][2 * kVariants][kCoopMaxPx + 1] = {};
+    int coop_bpc_tall[2 * kVariants] = {};  // the 64 x 80 prep-tile kernel at 10 px per lane
     unsigned* d_coop = nullptr;      // 2 counter sets of kCoopSetWords
     int32_t* d_status_out = nullptr; // [max_frames] host batch API: status per pair of the call
     int coop_par = 0;                // set used by the next coop call
@@ -2412,6 +2460,13 @@ struct youth_icp_ctx {
     double t_ms[3] = {0, 0, 0};
     int t_n[3] = {0, 0, 0};
 };
+
+// The kernels' template variant of a context: spec a7/a8 arithmetic in bit
+// 0, the lane32 reduction of spec a9 in bit 1.
+static int variant(const youth_icp_ctx* c)
+{
+    return c->spec | (c->reduce == YOUTH_REDUCE_LANE32 ? kRedLane32 : 0);
+}
 
 static int reduce_geometry(const youth_icp_ctx* c, int n_pairs, int* chunk_out)
 {
@@ -2605,11 +2660,15 @@ static int launch_reduce(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, P
     const bool fuse = fuse_it >= 0;
     if (assoc && fuse) return set_error(YOUTH_EINVAL, "launch_reduce: assoc with fused solve");
     const int sel = (assoc ? 8 : 0) | (fuse ? 4 : 0) | (c->fast ? 2 : 0) | (aligned ? 1 : 0);
-    if (c->spec == kSpecSurvey)
-        launch_reduce_sel<kSpecSurvey>(c, s, grid, dsrc, pm, thr2, chunk, ps, sel);
-    else
-        launch_reduce_sel<kSpecFma>(c, s, grid, dsrc, pm, thr2, chunk, ps, sel);
+    switch (variant(c)) {
+    case 0: launch_reduce_sel<0>(c, s, grid, dsrc, pm, thr2, chunk, ps, sel); break;
+    case 1: launch_reduce_sel<1>(c, s, grid, dsrc, pm, thr2, chunk, ps, sel); break;
+    case 2: launch_reduce_sel<2>(c, s, grid, dsrc, pm, thr2, chunk, ps, sel); break;
+    default: launch_reduce_sel<3>(c, s, grid, dsrc, pm, thr2, chunk, ps, sel); break;
+    }
     HIP_TRY(hipGetLastError());
+    c->lanes = youth_lanes{YOUTH_LANES_STRIDED, chunk, kRedThreads, 0};
+    c->has_lanes = true;
     *nblk_out = nb;
     return ev_end(c, s, &ep);
 }
@@ -2625,7 +2684,7 @@ static size_t coop_lds(int npx, int threads) { return (size_t)3 * npx * threads 
 static bool coop_plan(const youth_icp_ctx* c, int n_pairs, int* npx_out, int* G_out)
 {
     if (!c->coop || n_pairs > c->coop_max_pairs || n_pairs > kCoopMaxPairs) return false;
-    const int v = c->spec * 2 + (c->fast ? 1 : 0);
+    const int v = variant(c) * 2 + (c->fast ? 1 : 0);
     long long best = -1;
     for (int npx = 1; npx <= kCoopMaxPx; ++npx) {
         if (c->coop_px && npx != c->coop_px) continue;
@@ -2660,10 +2719,14 @@ static const void* coop_kernel_t(bool fast, int threads, bool tall)
                 : (const void*)k_icp_coop<kSp, false, 512, kCoopTileH>;
 }
 
-static const void* coop_kernel(int spec, bool fast, int threads, bool tall = false)
+static const void* coop_kernel(int var, bool fast, int threads, bool tall = false)
 {
-    return spec == kSpecSurvey ? coop_kernel_t<kSpecSurvey>(fast, threads, tall)
-                               : coop_kernel_t<kSpecFma>(fast, threads, tall);
+    switch (var) {
+    case 0: return coop_kernel_t<0>(fast, threads, tall);
+    case 1: return coop_kernel_t<1>(fast, threads, tall);
+    case 2: return coop_kernel_t<2>(fast, threads, tall);
+    default: return coop_kernel_t<3>(fast, threads, tall);
+    }
 }
 
 // Target frames to turn into records before (or, for the tracker, beside)
@@ -2712,7 +2775,7 @@ static CoopOrder g_coop_order[64];
 static int coop_enqueue(youth_icp_ctx* c, hipStream_t s, void** args, int blocks, int npx,
                         bool tall)
 {
-    const void* kern = coop_kernel(c->spec, c->fast, c->coop_threads, tall);
+    const void* kern = coop_kernel(variant(c), c->fast, c->coop_threads, tall);
     const dim3 grid((unsigned)blocks), block(c->coop_threads);
     const unsigned lds = (unsigned)coop_lds(npx, c->coop_threads);
     if (c->coop_refuse)  // test hook: the runtime's refusal, nothing enqueued
@@ -2768,7 +2831,7 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
     };
     const bool tall = c->coop_tile_src && c->coop_threads == 512 &&
                       npx * 512 == kTileW * kCoopTileHTall && G == tiles_of(kCoopTileHTall) &&
-                      (long long)n_pairs * G <= (long long)c->n_cu * c->coop_bpc_tall[c->spec * 2 + (c->fast ? 1 : 0)];
+                      (long long)n_pairs * G <= (long long)c->n_cu * c->coop_bpc_tall[variant(c) * 2 + (c->fast ? 1 : 0)];
     const bool tile_src = tall || (c->coop_tile_src && npx * c->coop_threads == kTileW * kCoopTileH &&
                                    G == tiles_of(kCoopTileH));
     CoopState cs{dTi,      c->d_T64, c->d_T32, c->d_status,          c->d_stats,
@@ -2800,20 +2863,23 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
     if (rc) return rc;
     c->last_coop_G = G;
     c->last_coop_px = npx;
+    c->lanes = youth_lanes{tile_src ? YOUTH_LANES_COOP_TILE : YOUTH_LANES_COOP, npx * c->coop_threads,
+                           c->coop_threads, npx};
+    c->has_lanes = true;
     return ev_end(c, s, &ep);
 }
 
-// k_icp<spec, fast, aligned> by index spec 4 + fast 2 + aligned
+// k_icp<variant, fast, aligned> by index variant 4 + fast 2 + aligned
 typedef void (*IcpKernel)(const int16_t*, const float4*, size_t, PairMap, int, int, Intr, FastK,
                           float, double*, IterState);
 static IcpKernel icp_kernel(int var)
 {
-    static const IcpKernel tab[8] = {
-        k_icp<kSpecFma, false, false>,    k_icp<kSpecFma, false, true>,
-        k_icp<kSpecFma, true, false>,     k_icp<kSpecFma, true, true>,
-        k_icp<kSpecSurvey, false, false>, k_icp<kSpecSurvey, false, true>,
-        k_icp<kSpecSurvey, true, false>,  k_icp<kSpecSurvey, true, true>};
-    return tab[var & 7];
+    static const IcpKernel tab[4 * kVariants] = {
+        k_icp<0, false, false>, k_icp<0, false, true>, k_icp<0, true, false>, k_icp<0, true, true>,
+        k_icp<1, false, false>, k_icp<1, false, true>, k_icp<1, true, false>, k_icp<1, true, true>,
+        k_icp<2, false, false>, k_icp<2, false, true>, k_icp<2, true, false>, k_icp<2, true, true>,
+        k_icp<3, false, false>, k_icp<3, false, true>, k_icp<3, true, false>, k_icp<3, true, true>};
+    return tab[var & (4 * kVariants - 1)];
 }
 
 // All ICP iterations of n_pairs pairs.  *exported is set when the kernel
@@ -2837,7 +2903,7 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
             !coop_plan(c, 1, &npx, &G) ||
             (long long)n_pairs * G >
                 (long long)c->n_cu *
-                    c->coop_bpc[c->coop_threads == 256][c->spec * 2 + (c->fast ? 1 : 0)][npx])
+                    c->coop_bpc[c->coop_threads == 256][variant(c) * 2 + (c->fast ? 1 : 0)][npx])
             return set_error(YOUTH_EINVAL, "track batch: %d pairs do not fit one cooperative grid",
                              n_pairs);
         coop = true;
@@ -2902,7 +2968,7 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
         rc = ensure_partials(c, (size_t)nb * n_pairs * kPartStride);
         if (rc) return rc;
         const bool aligned = (reinterpret_cast<uintptr_t>(dsrc) % 8 == 0) && (c->W % 4 == 0);
-        const int var = c->spec * 4 + (c->fast ? 2 : 0) + (aligned ? 1 : 0);
+        const int var = variant(c) * 4 + (c->fast ? 2 : 0) + (aligned ? 1 : 0);
         const long long items = (long long)iters * n_pairs * nb;
         long long grid = (long long)c->n_cu * c->icp_blocks_per_cu[var] / c->share;
         if (grid > items) grid = items;
@@ -2923,6 +2989,8 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kRedThreads), 0, s, dsrc, c->d_rec,
                            c->P, pm, c->W, c->H, c->K, c->F, thr2, c->d_partials, is);
         HIP_TRY(hipGetLastError());
+        c->lanes = youth_lanes{YOUTH_LANES_STRIDED, chunk, kRedThreads, 0};
+        c->has_lanes = true;
         rc = ev_end(c, s, &ep);
         if (rc) return rc;
     } else {
@@ -3031,6 +3099,28 @@ int youth_icp_set_spec(youth_icp_ctx* c, int spec)
     const int old = c->spec;
     c->spec = spec;
     return old;
+}
+
+int youth_icp_set_reduce(youth_icp_ctx* c, int mode)
+{
+    if (!c || (mode != YOUTH_REDUCE_EXACT && mode != YOUTH_REDUCE_LANE32))
+        return set_error(YOUTH_EINVAL, "set_reduce: bad arguments (%d)", mode);
+    const int old = c->reduce;
+    c->reduce = mode;
+    return old;
+}
+
+int youth_icp_get_reduce(const youth_icp_ctx* c)
+{
+    return c ? c->reduce : set_error(YOUTH_EINVAL, "get_reduce: null context");
+}
+
+int youth_icp_get_lanes(const youth_icp_ctx* c, youth_lanes* out)
+{
+    if (!c || !out) return set_error(YOUTH_EINVAL, "get_lanes: bad arguments");
+    if (!c->has_lanes) return set_error(YOUTH_EINVAL, "get_lanes: no align has run");
+    *out = c->lanes;
+    return YOUTH_OK;
 }
 
 int youth_icp_set_concurrency(youth_icp_ctx* c, int contexts)
@@ -3157,7 +3247,7 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess)
             return fail("hipGetDeviceProperties", e);
         c->n_cu = prop.multiProcessorCount;
-        for (int v = 0; v < 8; ++v) {
+        for (int v = 0; v < 4 * kVariants; ++v) {
             int nb = 0;
             if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
                      &nb, (const void*)icp_kernel(v), kRedThreads, 0)) != hipSuccess)
@@ -3169,7 +3259,7 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         const char* cth = getenv("YOUTH_ICP_COOP_THREADS");
         if (cth && atoi(cth) == 256) c->coop_threads = 256;
         for (int ti = 0; ti < 2; ++ti)
-            for (int v = 0; v < 4; ++v)
+            for (int v = 0; v < 2 * kVariants; ++v)
                 for (int npx = 1; npx <= kCoopMaxPx; ++npx) {
                     const int th = ti ? 256 : 512;
                     int nb = 0;
@@ -3179,7 +3269,7 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
                         return fail("occupancy coop", e);
                     c->coop_bpc[ti][v][npx] = nb;
                 }
-        for (int v = 0; v < 4; ++v) {
+        for (int v = 0; v < 2 * kVariants; ++v) {
             int nb = 0;
             const int npx = kTileW * kCoopTileHTall / 512;
             if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -3212,6 +3302,10 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         const char* sp = getenv("YOUTH_ICP_SPEC");
         if (sp && strcmp(sp, "survey") == 0) c->spec = kSpecSurvey;
         if (sp && strcmp(sp, "fma") == 0) c->spec = kSpecFma;
+        // spec a9 reduction: "lane32" (SURVEY §8a a9 as worded) or "exact"
+        const char* rd = getenv("YOUTH_ICP_REDUCE");
+        if (rd && strcmp(rd, "lane32") == 0) c->reduce = YOUTH_REDUCE_LANE32;
+        if (rd && strcmp(rd, "exact") == 0) c->reduce = YOUTH_REDUCE_EXACT;
     }
     if ((e = hipMalloc(&c->d_coop, 2 * kCoopSetWords * sizeof(unsigned))) != hipSuccess)
         return fail("hipMalloc coop", e);
@@ -3644,7 +3738,9 @@ static int batch_on_device(int dev, const int16_t* src, const int16_t* dst, int 
     }
     if (assoc_out) {
         int nb = 0;
+        const youth_lanes align_lanes = c->lanes;  // youth_icp_get_lanes reports the align's
         rc = launch_reduce(c, s, d_s, PairMap{0, 0}, n_pairs, true, &nb);
+        c->lanes = align_lanes;
         if (rc) return drain(rc);
         hipError_t e = hipMemcpyAsync(assoc_out, c->d_assoc, (size_t)n_pairs * N * sizeof(int32_t),
                                       hipMemcpyDeviceToHost, s);
@@ -3813,7 +3909,7 @@ static bool trk_chain_fits(const youth_icp_ctx* c, int m)
     if (!coop_plan(c, 1, &npx, &G)) return false;
     return (long long)m * G <=
            (long long)c->n_cu *
-               c->coop_bpc[c->coop_threads == 256][c->spec * 2 + (c->fast ? 1 : 0)][npx];
+               c->coop_bpc[c->coop_threads == 256][variant(c) * 2 + (c->fast ? 1 : 0)][npx];
 }
 
 // m consecutive host frames (m = 1, or a micro-batch that trk_chain_fits):
@@ -4064,7 +4160,7 @@ int youth_icp_track_set_batch(youth_icp_ctx* c, int frames)
     // submissions stay bit-identical
     c->coop_px = c->coop_px_env;
     if (frames > 1) {
-        const int v = c->spec * 2 + (c->fast ? 1 : 0);
+        const int v = variant(c) * 2 + (c->fast ? 1 : 0);
         for (int npx = 1; npx <= kCoopMaxPx; ++npx) {
             const long long G = (c->N + (long long)npx * c->coop_threads - 1) /
                                 ((long long)npx * c->coop_threads);

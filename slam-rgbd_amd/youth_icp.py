@@ -36,6 +36,9 @@ YOUTH_ENODEV = -4
 YOUTH_NEQ = 29
 SPEC_FMA = 0       # YOUTH_SPEC_FMA: opt-in, spec a7/a8 on fma chains
 SPEC_SURVEY = 1    # YOUTH_SPEC_SURVEY (default): SURVEY.md §8a a7/a8 as worded (no FMA, IEEE division)
+REDUCE_EXACT = 0   # YOUTH_REDUCE_EXACT: opt-in, every product exact in fp64
+REDUCE_LANE32 = 1  # YOUTH_REDUCE_LANE32 (default): SURVEY.md §8a a9, fp32 lanes -> fp64 finalize
+LANES_STRIDED, LANES_COOP, LANES_COOP_TILE = 0, 1, 2   # youth_lanes.kind
 STATUS_DEGENERATE = 1
 STATUS_FEW_MATCHES = 2
 
@@ -52,6 +55,14 @@ class Intrinsics(ctypes.Structure):
 
     def as_tuple(self):
         return (self.fx, self.fy, self.cx, self.cy, self.depth_scale)
+
+
+class Lanes(ctypes.Structure):
+    """youth_lanes: how one align partitioned an iteration's pixels into lanes."""
+    _fields_ = [("kind", c_int), ("chunk", c_int), ("threads", c_int), ("npx", c_int)]
+
+    def as_tuple(self):
+        return (self.kind, self.chunk, self.threads, self.npx)
 
 
 class Params(ctypes.Structure):
@@ -88,6 +99,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "youth_icp_set_spec": (c_int, [c_void_p, c_int]),
         "youth_icp_set_concurrency": (c_int, [c_void_p, c_int]),
         "youth_icp_get_spec": (c_int, [c_void_p]),
+        "youth_icp_set_reduce": (c_int, [c_void_p, c_int]),
+        "youth_icp_get_reduce": (c_int, [c_void_p]),
+        "youth_icp_get_lanes": (c_int, [c_void_p, POINTER(Lanes)]),
         "youth_icp_selftest_projquot": (c_int, [c_int, ctypes.c_longlong, ctypes.c_ulonglong,
                                                 POINTER(ctypes.c_longlong),
                                                 POINTER(ctypes.c_longlong),
@@ -312,7 +326,8 @@ class IcpContext:
     """Device workspace for W x H frames (youth_icp_create)."""
 
     def __init__(self, width: int, height: int, max_frames: int, K: Intrinsics | None = None,
-                 iters: int = 10, dist_thresh: float = 0.10, device: int = 0, spec=None):
+                 iters: int = 10, dist_thresh: float = 0.10, device: int = 0, spec=None,
+                 reduction=None):
         self._lib = load_library()
         self.W, self.H, self.max_frames = width, height, max_frames
         self.K = K if K is not None else default_intrinsics(width, height)
@@ -324,6 +339,8 @@ class IcpContext:
             raise IcpError(YOUTH_ENODEV if "no HIP device" in msg else YOUTH_EHIP, msg)
         if spec is not None:
             self.spec = spec
+        if reduction is not None:
+            self.reduction = reduction
 
     @property
     def handle(self) -> int:
@@ -343,6 +360,24 @@ class IcpContext:
     def spec(self, value) -> None:
         code = {"fma": SPEC_FMA, "survey": SPEC_SURVEY}.get(value, value)
         _check(self._lib.youth_icp_set_spec(self._ctx, int(code)))
+
+    @property
+    def reduction(self) -> int:
+        """Spec a9 reduction of the next aligns (REDUCE_LANE32 / REDUCE_EXACT)."""
+        return _check(self._lib.youth_icp_get_reduce(self._ctx))
+
+    @reduction.setter
+    def reduction(self, value) -> None:
+        code = {"exact": REDUCE_EXACT, "lane32": REDUCE_LANE32}.get(value, value)
+        _check(self._lib.youth_icp_set_reduce(self._ctx, int(code)))
+
+    def lanes(self) -> tuple:
+        """(kind, chunk, threads, npx) of the last align's lane partition
+        (youth_icp_get_lanes), the geometry oracle.set_reduce("lane32", ...)
+        restates."""
+        g = Lanes()
+        _check(self._lib.youth_icp_get_lanes(self._ctx, ctypes.byref(g)))
+        return g.as_tuple()
 
     def set_concurrency(self, contexts: int) -> int:
         """Declare `contexts` contexts aligning concurrently on this device

@@ -40,6 +40,30 @@ def _ensure_built():
 _ensure_built()
 
 
+def oracle_like(ctx_or_lanes):
+    """Context manager: the oracle's spec a9 reduction set to what a GPU
+    align ran.  Pass an IcpContext after its align (its reduction mode and
+    youth_icp_get_lanes partition), a lanes tuple (LANE32 with that
+    partition), or None (EXACT).  Inside it, oracle.reduce / align /
+    align_batch restate the GPU's sums lane for lane (fp32 lane sums, fp64
+    finalize), so correspondence counts compare exactly and sums to fp64
+    summation order."""
+    import oracle
+    import youth_icp
+    lanes = ctx_or_lanes
+    if isinstance(ctx_or_lanes, youth_icp.IcpContext):
+        lanes = ctx_or_lanes.lanes() if ctx_or_lanes.reduction == youth_icp.REDUCE_LANE32 else None
+    if lanes is None:
+        return oracle.reduction("exact")
+    return oracle.reduction("lane32", lanes)
+
+
+def lanes_of(ctx):
+    """The context's last-align partition, or None when it ran EXACT."""
+    import youth_icp
+    return ctx.lanes() if ctx.reduction == youth_icp.REDUCE_LANE32 else None
+
+
 @pytest.fixture(scope="session")
 def has_gpu():
     import youth_icp

@@ -15,7 +15,7 @@ import pytest
 import oracle
 import youth_icp
 import youth_synth
-from conftest import GOLDEN
+from conftest import GOLDEN, lanes_of, oracle_like
 
 pytestmark = pytest.mark.gpu
 
@@ -107,7 +107,8 @@ def test_assoc_and_reduce_match_golden(name):
     g = _load(name)
     K = _K(g["K"])
     H, W = g["src"].shape
-    with youth_icp.IcpContext(W, H, 2, K=K, dist_thresh=float(g["dist_thresh"])) as ctx:
+    with youth_icp.IcpContext(W, H, 2, K=K, dist_thresh=float(g["dist_thresh"]),
+                              reduction="exact") as ctx:     # the fixtures' reduction
         I12 = np.eye(4, dtype=np.float32)[:3]
         assoc, neq = ctx.reduce(g["src"], g["dst"], I12)
         assert np.array_equal(assoc, g["idx_identity"])
@@ -127,7 +128,8 @@ def test_assoc_bit_exact_every_iteration_640x480():
             T32 = T[:3].astype(np.float32)
             g_idx, g_neq = ctx.reduce(src, dst, T32)
             o_idx = oracle.associate(src, dst, T32, K)
-            o_neq = oracle.reduce(src, dst, T32, K)
+            with oracle_like(ctx):
+                o_neq = oracle.reduce(src, dst, T32, K)
             assert np.array_equal(g_idx, o_idx), it
             np.testing.assert_allclose(g_neq, o_neq, rtol=1e-11, atol=1e-9)
             xi, st = oracle.solve(o_neq)
@@ -289,9 +291,11 @@ def test_context_device_api_poses_and_stats():
         T64, T32, st = ctx.get_poses(n)
         cnt, r2 = ctx.get_stats(n, 10)
         Tdev = out.cpu().numpy().reshape(n, 4, 4)
+        lanes = lanes_of(ctx)
         del lib, ctypes
     for p in range(n):
-        T64o, _, sto, stats = oracle.align(src[p], dst[p], iters=10)
+        with oracle_like(lanes):
+            T64o, _, sto, stats = oracle.align(src[p], dst[p], iters=10)
         assert _pose_err(T64[p], T64o) <= POSE_TOL
         assert np.array_equal(Tdev[p], T32[p]) and np.array_equal(Tdev[p], Tb[p])
         assert st[p] == sto
@@ -325,9 +329,11 @@ def test_single_pair_coop_tile_sources(tile_src, monkeypatch):
             T64, _, st = ctx.get_poses(1)
             cnt, _ = ctx.get_stats(1, iters)
             plan = ctx.get_plan()
+            lanes = lanes_of(ctx)
         assert plan["kernel"] == "k_icp_coop" and plan["workgroups_per_pair"] == G
         assert plan["px_per_lane"] == px
-        To, _, sto, stats = oracle.align(src[0], dst[0], iters=iters)
+        with oracle_like(lanes):
+            To, _, sto, stats = oracle.align(src[0], dst[0], iters=iters)
         assert st[0] == sto and _pose_err(T64[0], To) <= POSE_TOL
         assert np.array_equal(cnt[0], stats[:, 0])
 
@@ -388,14 +394,17 @@ def test_sequence_c5_workload_640x480():
         ctx.sync()
         T64, T32, st = ctx.get_poses(F - 1)
         cnt, _ = ctx.get_stats(F - 1, 10)
-        T_cpu, st_cpu = oracle.align_batch(frames[1:], frames[:-1], iters=10,
-                                           n_threads=min(16, os.cpu_count() or 1))
+        lanes = lanes_of(ctx)
+        with oracle_like(lanes):
+            T_cpu, st_cpu = oracle.align_batch(frames[1:], frames[:-1], iters=10,
+                                               n_threads=min(16, os.cpu_count() or 1))
         assert np.array_equal(st, st_cpu) and not st.any()
         err = [_pose_err(T64[k], T_cpu[k]) for k in range(F - 1)]
         assert max(err) <= POSE_TOL, int(np.argmax(err))
         K = oracle.viewer_K(640, 480)
         for k in (0, 1, 77, 150, F - 2):
-            _, _, _, stats = oracle.align(frames[k + 1], frames[k], iters=10)
+            with oracle_like(lanes):
+                _, _, _, stats = oracle.align(frames[k + 1], frames[k], iters=10)
             assert np.array_equal(cnt[k], stats[:, 0]), k
             g_idx, _ = ctx.reduce(frames[k + 1], frames[k], T32[k][:3])
             assert np.array_equal(g_idx, oracle.associate(frames[k + 1], frames[k], T32[k][:3], K))
@@ -420,16 +429,19 @@ def test_sequence_c5_full_length_one_call():
         ctx.sync()
         T64, T32, st = ctx.get_poses(F - 1)
         cnt, _ = ctx.get_stats(F - 1, 10)
+        lanes = lanes_of(ctx)
     del d
-    T_cpu, st_cpu = oracle.align_batch(frames[1:], frames[:-1], iters=10,
-                                       n_threads=min(16, os.cpu_count() or 1))
+    with oracle_like(lanes):
+        T_cpu, st_cpu = oracle.align_batch(frames[1:], frames[:-1], iters=10,
+                                           n_threads=min(16, os.cpu_count() or 1))
     assert np.array_equal(st, st_cpu) and not st.any()
     err = [_pose_err(T64[k], T_cpu[k]) for k in range(F - 1)]
     assert max(err) <= POSE_TOL, (int(np.argmax(err)), max(err))
     K = oracle.viewer_K(640, 480)
     with youth_icp.IcpContext(640, 480, 2) as one:
         for k in (0, 255, 256, 511, 880, 998):
-            _, _, _, stats = oracle.align(frames[k + 1], frames[k], iters=10)
+            with oracle_like(lanes):
+                _, _, _, stats = oracle.align(frames[k + 1], frames[k], iters=10)
             assert np.array_equal(cnt[k], stats[:, 0]), k
             if k in (0, 880, 998):
                 g_idx, _ = one.reduce(frames[k + 1], frames[k], T32[k][:3])
@@ -742,10 +754,12 @@ def test_kernel_paths_match_oracle(monkeypatch, mode):
         plan = ctx.get_plan()
         T64, T32, st = ctx.get_poses(n)
         cnt, _ = ctx.get_stats(n, 10)
+        lanes = lanes_of(ctx)
     assert plan["kernel"] == PLAN[mode]
     Tdev = out.cpu().numpy().reshape(n, 4, 4)
     for p in range(n):
-        T64o, _, sto, stats = oracle.align(src[p], dst[p], iters=10)
+        with oracle_like(lanes):
+            T64o, _, sto, stats = oracle.align(src[p], dst[p], iters=10)
         assert st[p] == sto == 0
         assert _pose_err(T64[p], T64o) <= POSE_TOL
         assert np.array_equal(Tdev[p], T32[p])
@@ -908,10 +922,12 @@ def test_headline_512_pairs_one_launch():
         T64, T32, st = ctx.get_poses(n)
         cnt, r2 = ctx.get_stats(n, 10)
         Tout = out.cpu().numpy().reshape(n, 4, 4)
+        lanes = lanes_of(ctx)
     del ds, dd
-    T_cpu, st_cpu, stats = oracle.align_batch(src, dst, iters=10,
-                                              n_threads=min(16, os.cpu_count() or 1),
-                                              want_stats=True)
+    with oracle_like(lanes):
+        T_cpu, st_cpu, stats = oracle.align_batch(src, dst, iters=10,
+                                                  n_threads=min(16, os.cpu_count() or 1),
+                                                  want_stats=True)
     assert not st.any() and not st_cpu.any()
     err = np.abs(T64[:, :3, :4] - T_cpu[:, :3, :4]).max(axis=(1, 2))
     assert float(err.max()) <= POSE_TOL, (int(err.argmax()), float(err.max()))
@@ -946,6 +962,7 @@ def test_concurrent_contexts_share_the_device():
     streams = [torch.cuda.Stream() for _ in range(2)]
     torch.cuda.synchronize()
     ctxs = [youth_icp.IcpContext(W, H, n, iters=10) for _ in range(2)]
+    lanes = [None, None]
     try:
         for c in ctxs:
             with pytest.raises(youth_icp.IcpError):
@@ -967,15 +984,17 @@ def test_concurrent_contexts_share_the_device():
                 cnt, _ = ctxs[q].get_stats(n, 10)
                 assert np.array_equal(outs[q].cpu().numpy().reshape(n, 4, 4), T32)
                 res.append((T64, st, cnt))
+                lanes[q] = lanes_of(ctxs[q])
             got.append(res)
         assert ctxs[0].set_concurrency(1) == 2
     finally:
         for c in ctxs:
             c.close()
     for q, (src, dst) in enumerate(batches):
-        T_cpu, st_cpu, stats = oracle.align_batch(src, dst, iters=10,
-                                                  n_threads=min(16, os.cpu_count() or 1),
-                                                  want_stats=True)
+        with oracle_like(lanes[q]):
+            T_cpu, st_cpu, stats = oracle.align_batch(src, dst, iters=10,
+                                                      n_threads=min(16, os.cpu_count() or 1),
+                                                      want_stats=True)
         T64, st, cnt = got[0][q]
         assert not st.any() and not st_cpu.any()
         err = np.abs(T64[:, :3, :4] - T_cpu[:, :3, :4]).max()

@@ -24,7 +24,7 @@ import torch
 import oracle
 import youth_icp
 import youth_synth
-from conftest import GOLDEN
+from conftest import GOLDEN, lanes_of, oracle_like
 
 pytestmark = pytest.mark.gpu
 POSE_TOL = 1e-5
@@ -70,7 +70,8 @@ def test_golden_fixtures_per_spec(name, spec):
     K = youth_icp.Intrinsics(*[float(v) for v in g["K"]])
     H, W = g["src"].shape
     it, d = int(g["iters"]), float(g["dist_thresh"])
-    with youth_icp.IcpContext(W, H, 4, K=K, iters=it, dist_thresh=d, spec=spec) as ctx:
+    with youth_icp.IcpContext(W, H, 4, K=K, iters=it, dist_thresh=d, spec=spec,
+                              reduction="exact") as ctx:    # the fixtures' reduction
         assoc, neq = ctx.reduce(g["src"], g["dst"], np.eye(4, dtype=np.float32)[:3])
         assert np.array_equal(assoc, g["idx_identity"])
         np.testing.assert_allclose(neq, g["neq_identity"], rtol=1e-12, atol=1e-12)
@@ -87,7 +88,8 @@ def test_golden_fixtures_per_spec(name, spec):
         assert np.array_equal(cnt[0], g["stats"][:, 0])
     os.environ["YOUTH_ICP_NO_COOP"] = "1"
     try:
-        with youth_icp.IcpContext(W, H, 4, K=K, iters=it, dist_thresh=d, spec=spec) as ctx:
+        with youth_icp.IcpContext(W, H, 4, K=K, iters=it, dist_thresh=d, spec=spec,
+                              reduction="exact") as ctx:    # the fixtures' reduction
             ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), 4)
             T4, _, s4 = ctx.get_poses(4)
             cnt, _ = ctx.get_stats(4, it)
@@ -115,7 +117,8 @@ def test_assoc_bit_exact_every_iteration_640x480(spec):
             T32 = T[:3].astype(np.float32)
             g_idx, g_neq = ctx.reduce(src, dst, T32)
             assert np.array_equal(g_idx, oracle.associate(src, dst, T32, K)), it
-            o_neq = oracle.reduce(src, dst, T32, K)
+            with oracle_like(ctx):
+                o_neq = oracle.reduce(src, dst, T32, K)
             np.testing.assert_allclose(g_neq, o_neq, rtol=1e-11, atol=1e-9)
             xi, st = oracle.solve(o_neq)
             assert st == 0
@@ -130,8 +133,9 @@ def test_assoc_bit_exact_every_iteration_640x480(spec):
             T32 = Tr[:3].astype(np.float32)
             g_idx, g_neq = ctx.reduce(s[0], t[0], T32)
             assert np.array_equal(g_idx, oracle.associate(s[0], t[0], T32, K)), draw
-            np.testing.assert_allclose(g_neq, oracle.reduce(s[0], t[0], T32, K), rtol=1e-11,
-                                       atol=1e-9, err_msg=str(draw))
+            with oracle_like(ctx):
+                o_neq = oracle.reduce(s[0], t[0], T32, K)
+            np.testing.assert_allclose(g_neq, o_neq, rtol=1e-11, atol=1e-9, err_msg=str(draw))
 
 
 @pytest.mark.parametrize("spec", SPECS)
@@ -161,7 +165,8 @@ def test_assoc_extreme_poses(spec):
             g_idx, g_neq = ctx.reduce(src[0], dst[0], T32)
             o_idx = oracle.associate(src[0], dst[0], T32, K)
             assert np.array_equal(g_idx, o_idx), draw
-            o_neq = oracle.reduce(src[0], dst[0], T32, K)
+            with oracle_like(ctx):
+                o_neq = oracle.reduce(src[0], dst[0], T32, K)
             assert g_neq[28] == o_neq[28], draw
             np.testing.assert_allclose(g_neq, o_neq, rtol=1e-11, atol=1e-9, err_msg=str(draw))
             Ts.append(Tr)
@@ -215,12 +220,15 @@ def test_align_all_kernel_paths_per_spec(W, H, iters, n, spec):
         T64, _, st = ctx.get_poses(n)
         cnt, _ = ctx.get_stats(n, iters)
         plan = ctx.get_plan()
+        lanes = lanes_of(ctx)
     if n == 1:
         assert plan["kernel"] == "k_icp_coop"
     if n == 64:
         assert plan["kernel"].startswith("k_prep + k_icp")
-    T_cpu, st_cpu, stats = oracle.align_batch(src, dst, K=oracle.viewer_K(W, H), iters=iters,
-                                              n_threads=min(n, 16), want_stats=True)
+    with oracle_like(lanes):
+        T_cpu, st_cpu, stats = oracle.align_batch(src, dst, K=oracle.viewer_K(W, H),
+                                                  iters=iters, n_threads=min(n, 16),
+                                                  want_stats=True)
     assert np.array_equal(st, st_cpu) and not st.any()
     assert _err(T64, T_cpu) <= POSE_TOL
     assert np.array_equal(cnt, stats[..., 0])

@@ -216,3 +216,98 @@ def test_world_frame_viewer_list_equals_numpy():
     got = oracle.viewer_cloud(d, None, K, T_world=T)
     assert np.array_equal(got[:, :3].view(np.uint32), want.view(np.uint32))
     assert not got[:, 3:].any()
+
+
+# --------------------------------------------------- spec a9, lane32 mode --
+def lane_np(kind, chunk, threads, npx, W, H):
+    """Lane of every pixel (raster index) under a launch's partition, from
+    include/youth_icp.h's description of youth_lanes."""
+    i = np.arange(W * H, dtype=np.int64)
+    T = threads
+    if kind == oracle.LANES_STRIDED:
+        c, o = i // chunk, i % chunk
+        return c * T + (o % (4 * T)) // 4
+    if kind == oracle.LANES_COOP:
+        C = npx * T
+        return (i // C) * T + (i % C) % T
+    th = npx * T // 64
+    u, v = i % W, i // W
+    tx, ty = u // 64, v // th
+    k = (v - ty * th) * 64 + (u - tx * 64)
+    return (ty * ((W + 63) // 64) + tx) * T + k % T
+
+
+def reduce_lane32_np(S, Tg, Nt, T12, K, thr, lanes, spec):
+    """SURVEY §8a a9 as worded: per lane, fp32 sums (fma32, from +0, pixel
+    order) of the matched pixels' 28 products; then the lanes' sums in fp64,
+    in lane order; the count exact."""
+    idx, (qx, qy, qz) = associate_np(S, Tg, Nt, T12, K, thr, spec)
+    H, W = S[2].shape
+    m = idx >= 0
+    j = idx[m]
+    tX, tY, tZ = (a.ravel()[j] for a in Tg)
+    nx, ny, nz = (a.ravel()[j] for a in Nt)
+    q0, q1, q2 = qx[m], qy[m], qz[m]
+    dx, dy, dz = q0 - tX, q1 - tY, q2 - tZ
+    if spec == "survey":
+        r = (nx * dx + ny * dy) + nz * dz
+        J = [q1 * nz - q2 * ny, q2 * nx - q0 * nz, q0 * ny - q1 * nx, nx, ny, nz]
+    else:
+        r = fma32(nz, dz, fma32(ny, dy, nx * dx))
+        J = [fma32(q1, nz, -(q2 * ny)), fma32(q2, nx, -(q0 * nz)), fma32(q0, ny, -(q1 * nx)),
+             nx, ny, nz]
+    pairs = [(J[a], J[b]) for a in range(6) for b in range(a, 6)]
+    pairs += [(J[a], r) for a in range(6)] + [(r, r)]
+    lane = lane_np(*lanes, W, H)[m]
+    n_lanes = int(lane_np(*lanes, W, H).max()) + 1
+    order = np.argsort(lane, kind="stable")          # within a lane: pixel order
+    ls = lane[order]
+    first = np.r_[0, np.flatnonzero(np.diff(ls)) + 1]
+    rank = np.arange(ls.size) - np.repeat(first, np.diff(np.r_[first, ls.size]))
+    acc = np.zeros((n_lanes, 28), f32)
+    for step in range(int(rank.max()) + 1 if rank.size else 0):
+        sel = order[rank == step]
+        L = lane[sel]
+        for k, (a, b) in enumerate(pairs):
+            acc[L, k] = fma32(a[sel], b[sel], acc[L, k])
+    out = np.zeros(29, f64)
+    for k in range(28):
+        out[k] = np.cumsum(np.r_[0.0, acc[:, k].astype(f64)])[-1]
+    out[28] = float(m.sum())
+    return out
+
+
+@pytest.mark.parametrize("spec", ["fma", "survey"])
+@pytest.mark.parametrize("lanes", [(0, 2048, 256, 0), (0, 51200, 256, 0), (1, 0, 512, 3),
+                                   (2, 0, 512, 3), (2, 0, 512, 10)],
+                         ids=["strided2048", "strided51200", "coop3", "tile64x24", "tile64x80"])
+def test_lane32_restatement_equals_oracle_bitwise(lanes, spec):
+    """oracle_set_reduce(LANE32, partition) against the numpy restatement
+    above, bit for bit, at 640x480 (the partitions k_icp, k_icp_coop and the
+    tall-tile kernel use) and at a larger motion; and LANE32 against EXACT
+    within the fp32 rounding of the lane sums."""
+    src, dst, _ = youth_synth.pairs(7, 1, 640, 480)
+    K = oracle.viewer_K(640, 480)
+    S, Tg = backproject_np(src[0], K), backproject_np(dst[0], K)
+    Nt = normals_np(*Tg)
+    th = np.deg2rad(2.0)
+    R = np.array([[np.cos(th), 0, np.sin(th)], [0, 1, 0], [-np.sin(th), 0, np.cos(th)]])
+    for T in (np.eye(4)[:3], np.hstack([R, [[0.02], [0.01], [-0.01]]])):
+        T12 = T.astype(f32)
+        want = reduce_lane32_np(S, Tg, Nt, T12, K, 0.10, lanes, spec)
+        with oracle.spec(spec), oracle.reduction("lane32", lanes):
+            got = oracle.reduce(src[0], dst[0], T12, K)
+        with oracle.spec(spec):
+            exact = oracle.reduce(src[0], dst[0], T12, K)
+        assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+        assert got[28] == exact[28] > 0
+        assert np.abs(got[:28] - exact[:28]).max() <= 1e-4 * np.abs(exact[:28]).max()
+    assert oracle.get_reduce() == oracle.REDUCE_EXACT
+
+
+def test_lane32_rejects_bad_partitions():
+    for mode, lanes in (("lane32", None), ("lane32", (0, 0, 256, 0)), ("lane32", (0, 2048, 100, 0)),
+                        ("lane32", (1, 0, 512, 0)), ("lane32", (7, 2048, 256, 1)), (3, None)):
+        with pytest.raises(ValueError):
+            oracle.set_reduce(mode, lanes)
+    assert oracle.get_reduce() == oracle.REDUCE_EXACT
