@@ -29,6 +29,7 @@ Launch: python bench.py [--gpus N] [--steps K] [--warmup W]   (N > 1: bench.py s
 Rank 0 prints ONE JSON line.
 """
 import argparse
+import ctypes
 import hashlib
 import json
 import math
@@ -850,7 +851,7 @@ def streamed_rate(a, frames, rel_batch, passes=5):
     # submissions in flight; per m, the poses must equal track_frame's in the
     # same plan bit for bit
     by_size, equal, launches, diff_vs_default = {}, True, {}, 0.0
-    best_m, Tb_best = None, None
+    best_m, Tb_best, sync_by_m = None, None, {}
     for m in sorted({2, youth_icp.TRACK_MAX_BATCH // 2, youth_icp.TRACK_MAX_BATCH}):
         ctx2 = youth_icp.IcpContext(a.width, a.height, 2 * m, iters=a.iters)
         ctx2.track_set_batch(m)
@@ -866,6 +867,7 @@ def streamed_rate(a, frames, rel_batch, passes=5):
         sync_b = [T for T, _, has in (ctx2.track_frame(f) for f in frames) if has]
         plan_b = ctx2.get_plan()
         ctx2.close()
+        sync_by_m[m] = np.stack(sync_b)
         equal &= bool(np.array_equal(Tb, np.stack(sync_b)))
         diff_vs_default = max(diff_vs_default, pose_err(Tb, np.stack(sync)))
         by_size[m] = {"value": float(np.median(r_b)), "pass_values": r_b,
@@ -875,7 +877,8 @@ def streamed_rate(a, frames, rel_batch, passes=5):
             best_m, Tb_best = m, Tb
     v1, vp, vs = float(np.median(r_c)), float(np.median(r_py)), float(np.median(r_sync))
     vb = by_size[best_m]["value"]
-    return {"frames": n, "value": max(v1, vb), "unit": "frames/s",
+    slam = slam_api_rate(a, frames, sync_by_m.get(youth_icp.TRACK_MAX_BATCH), passes=passes)
+    return {"frames": n, "value": max(v1, vb), "unit": "frames/s", "slam_api": slam,
             "us_per_frame": 1e6 / max(v1, vb),
             "mode": f"micro-batches of {best_m} frames" if vb >= v1 else "one launch per frame",
             "batched_value": vb, "batched_frames_per_launch": best_m,
@@ -899,6 +902,75 @@ def streamed_rate(a, frames, rel_batch, passes=5):
                     "track_frame's in its plan bit for bit (batched_equals_sync); "
                     "python_pipelined_value: track_submit/collect from Python, one launch per "
                     "frame; sync_value: track_frame"}
+
+
+def slam_api_rate(a, frames, rel_plan, passes=5):
+    """The drop-in path itself (SLAM.cpp:126-175 / :32-63 semantics):
+    processSlamFrame from one producer thread into the module's ingest queue,
+    the module's worker tracking in micro-batches (its default: as many
+    queued frames as YOUTH_TRACK_MAX_BATCH per launch, page-locked queue
+    buffers submitted in place).  Backlogged: the producer pushes as fast as
+    it can but never past the reference's drop threshold (it waits while 10
+    frames are queued, so nothing is dropped); timed until the last frame's
+    pose is in the trajectory (median of `passes`).  Live: one frame at a
+    time, each waited for (the per-frame latency a camera at 30 fps sees).
+    World poses checked against the prefix product of track_frame's relative
+    poses on a context with the worker's plan (rel_plan: same frames,
+    youth_icp_track_set_batch(YOUTH_TRACK_MAX_BATCH)), and the micro-batch
+    count (youth_slam_batched_frames)."""
+    lib = youth_icp.load_library()
+    n = frames.shape[0]
+    fr = np.ascontiguousarray(frames, np.int16)
+    ptrs = [fr[f].ctypes.data_as(ctypes.POINTER(ctypes.c_int16)) for f in range(n)]
+    H, W = fr.shape[1:]
+    youth_icp.initSlamModule(None)
+    out = {"frames": n, "producer": "one Python thread, ctypes processSlamFrame",
+           "worker_batch": os.environ.get("YOUTH_SLAM_TRACK_BATCH",
+                                          str(youth_icp.TRACK_MAX_BATCH))}
+    try:
+        for f in range(min(n, 24)):                   # warm: context, plan, page-locked pool
+            lib.processSlamFrame(ptrs[f], None, W, H, f)
+        youth_icp.slam_wait_idle(20000)
+        rates, batched = [], []
+        for _ in range(passes):
+            youth_icp.resetSlam()
+            youth_icp.slam_wait_idle(20000)
+            b0 = youth_icp.slam_batched_frames()
+            t0 = time.perf_counter()
+            for f in range(n):
+                while lib.youth_slam_queue_size() >= 10:
+                    pass
+                lib.processSlamFrame(ptrs[f], None, W, H, f)
+            while lib.youth_slam_trajectory_length() < n:
+                pass
+            rates.append(n / (time.perf_counter() - t0))
+            batched.append(youth_icp.slam_batched_frames() - b0)
+        ts, T = youth_icp.slam_trajectory()
+        out.update({"value": float(np.median(rates)), "unit": "frames/s",
+                    "pass_values": rates, "batched_frames_per_pass": batched,
+                    "frames_recorded": int(len(ts)), "timestamps_in_order":
+                    bool(np.array_equal(ts, np.arange(n, dtype=np.uint32)))})
+        if rel_plan is not None:
+            acc = np.eye(4)
+            err = 0.0
+            for k in range(1, min(len(T), rel_plan.shape[0] + 1)):
+                acc = acc @ rel_plan[k - 1]
+                err = max(err, pose_err(T[k], acc))
+            out["world_pose_max_abs_diff_vs_track_frame_plan"] = err
+        youth_icp.resetSlam()
+        youth_icp.slam_wait_idle(20000)
+        lat = []
+        for f in range(min(n, 60)):
+            t0 = time.perf_counter()
+            lib.processSlamFrame(ptrs[f], None, W, H, f)
+            while lib.youth_slam_trajectory_length() < f + 1:
+                pass
+            lat.append((time.perf_counter() - t0) * 1e6)
+        out["live_latency_us_median"] = float(np.median(lat[1:]))
+        out["live_latency_us_p90"] = float(np.percentile(lat[1:], 90))
+    finally:
+        youth_icp.stopSlamModule()
+    return out
 
 
 def survey_noise_parity(a, ctx, main, n=16):

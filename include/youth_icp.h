@@ -381,9 +381,9 @@ int youth_icp_track_frame(youth_icp_ctx* ctx, const int16_t* depth,
  * submitted frame and returns exactly what youth_icp_track_frame would have
  * returned for it (status bits or a negative code, T_rel, *has_ref).
  * youth_icp_track_frame = submit + collect, with nothing in flight.
- * The first tracking call of a context pins YOUTH_TRACK_MAX_IN_FLIGHT
- * staging frames of host memory (W x H x 2 bytes each: 9.8 MB at 640x480),
- * freed by youth_icp_destroy. */
+ * Each frame in flight pins one staging frame of host memory (W x H x 2
+ * bytes: 614 KB at 640x480), allocated the first time the ring needs that
+ * many and freed by youth_icp_destroy. */
 #define YOUTH_TRACK_MAX_IN_FLIGHT 16
 int youth_icp_track_submit(youth_icp_ctx* ctx, const int16_t* depth,
                            const double* T_init);
@@ -407,6 +407,19 @@ int youth_icp_track_pending(const youth_icp_ctx* ctx);
 #define YOUTH_TRACK_MAX_BATCH 8
 int youth_icp_track_submit_batch(youth_icp_ctx* ctx, const int16_t* depth, int n_frames);
 
+/* youth_icp_track_submit_batch without the staging copy: frames[i] (n_frames
+ * pointers) are page-locked host frames the caller allocated with
+ * youth_icp_host_alloc and keeps unchanged until frame i has been collected;
+ * their H2D copies read them in place.  The SLAM worker submits the ingest
+ * queue's buffers this way, so a frame is copied once on the host (in
+ * processSlamFrame).  Same results and limits as youth_icp_track_submit_batch. */
+int youth_icp_track_submit_pinned(youth_icp_ctx* ctx, const int16_t* const* frames,
+                                  int n_frames);
+/* Page-locked host memory for `values` int16 values (NULL on failure or 0),
+ * and its release (NULL is ignored). */
+int16_t* youth_icp_host_alloc(size_t values);
+void youth_icp_host_free(int16_t* p);
+
 /* Frames per submission youth_icp_track_host_sequence uses (1, default: one
  * launch per frame; up to YOUTH_TRACK_MAX_BATCH: micro-batches).  Batch mode
  * (> 1) plans the context's cooperative launches with the fewest source
@@ -419,6 +432,9 @@ int youth_icp_track_set_batch(youth_icp_ctx* ctx, int frames);
 /* Micro-batch launches this context has run (a batch that did not fit one
  * grid runs as per-frame launches and is not counted). */
 long long youth_icp_track_chained(const youth_icp_ctx* ctx);
+/* Frames those micro-batch launches aligned (the first frame of a sequence,
+ * prepped alone, and frames that ran one launch each are not counted). */
+long long youth_icp_track_chained_frames(const youth_icp_ctx* ctx);
 
 /* A recorded host sequence (frames [n_frames][H][W], e.g. a .bin playback)
  * through the tracker, two frames in flight (with youth_icp_track_set_batch(m):
@@ -472,10 +488,15 @@ int youth_slam_get_pose(int index, uint32_t* timestamp, double* T_wc);
 /* Block until the ingest queue is empty and the worker is idle, or
  * timeout_ms elapses.  Returns 1 when drained, 0 on timeout / not running. */
 int youth_slam_wait_idle(int timeout_ms);
-/* Frames the worker has submitted in micro-batches that ran as chained
- * launches since the module started (YOUTH_SLAM_TRACK_BATCH=m >= 2 with a
- * backlogged queue; 0 otherwise). */
+/* Frames the worker has aligned in chained micro-batch launches since the
+ * module started (youth_icp_track_chained_frames of its context: frames of
+ * a backlogged queue; 0 when every frame arrived alone or with
+ * YOUTH_SLAM_TRACK_BATCH=1). */
 long long youth_slam_batched_frames(void);
+/* Frames waiting in the module's ingest queue (processSlamFrame drops the
+ * oldest down to 5 when it passes 10, SLAM.cpp:163-168): a producer that
+ * must not lose frames waits while this is 10. */
+int youth_slam_queue_size(void);
 /* Block until the module stops (used by algorithmModule). */
 void youth_slam_wait_stopped(void);
 

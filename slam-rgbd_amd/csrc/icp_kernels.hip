@@ -2428,6 +2428,7 @@ struct youth_icp_ctx {
     bool coop_tile_src = true;        // YOUTH_ICP_COOP_TILE_SRC=0: contiguous source chunks
     int trk_batch = 1;                // frames per submission in youth_icp_track_host_sequence
     long long trk_chained = 0;        // micro-batch launches so far (youth_icp_track_chained)
+    long long trk_chained_frames = 0; // frames those launches aligned (youth_icp_track_chained_frames)
     int queues = 0;                  // k_icp work queues (YOUTH_ICP_QUEUES=1..8; 0: by batch size)
     int share = 1;                   // contexts launching k_icp concurrently (set_concurrency)
     int prep_xcd_map = 0;             // YOUTH_ICP_PREP_XCD_MAP=1: k_prep tiles contiguous per XCD (slower)
@@ -3872,10 +3873,10 @@ static void track_grow(youth_icp_ctx* c, int need)
     c->trk_cap = std::min(kTrackDepth, need);
 }
 
-static int track_entry_pinned(youth_icp_ctx* c, int e)
+static int track_entry_pinned(youth_icp_ctx* c, int e, bool staging)
 {
     auto& q = c->trk[e];
-    if (!q.pinned)
+    if (staging && !q.pinned)
         HIP_TRY(hipHostMalloc((void**)&q.pinned, (size_t)c->N * sizeof(int16_t),
                               hipHostMallocDefault));
     if (!q.res) HIP_TRY(hipHostMalloc((void**)&q.res, 17 * sizeof(double), hipHostMallocCoherent));
@@ -3919,8 +3920,10 @@ static bool trk_chain_fits(const youth_icp_ctx* c, int m)
 // single-pair align with the fused prep of the new frame, or the chained
 // micro-batch (pair i aligns frame i to frame i-1, frame -1 = the
 // reference).  One completion event for the launch, shared by its entries.
+// frames (nullable): the m frames are the caller's page-locked buffers,
+// copied H2D in place (no staging copy; youth_icp_track_submit_pinned).
 static int track_submit_frames(youth_icp_ctx* c, const int16_t* depth, int m,
-                               const double* T_init)
+                               const double* T_init, const int16_t* const* frames = nullptr)
 {
     hipStream_t s = c->stream;
     const size_t N = c->N;
@@ -3937,20 +3940,21 @@ static int track_submit_frames(youth_icp_ctx* c, const int16_t* depth, int m,
     track_grow(c, c->trk_n + m);
     for (int i = 0; i < m; ++i) {
         qi[i] = (c->trk_head + c->trk_n + i) % c->trk_cap;
-        const int rc = track_entry_pinned(c, qi[i]);  // before anything is enqueued
+        const int rc = track_entry_pinned(c, qi[i], !frames);  // before anything is enqueued
         if (rc) return rc;
     }
     auto& ql = c->trk[qi[m - 1]];
     // the caller's buffers are free on return: copy into the entries' pinned
     // staging, then H2D after the last launch that read these depth slots
     for (int i = 0; i < m; ++i) {
-        memcpy(c->trk[qi[i]].pinned, depth + (size_t)i * N, N * sizeof(int16_t));
+        if (!frames) memcpy(c->trk[qi[i]].pinned, depth + (size_t)i * N, N * sizeof(int16_t));
         const int last = c->trk_dslot_last[d0 + i];
         if (last >= 0) HIP_TRY(hipStreamWaitEvent(c->xfer, c->trk[last].ev, 0));
     }
     for (int i = 0; i < m; ++i)
-        HIP_TRY(hipMemcpyAsync(c->d_depth + (size_t)(d0 + i) * N, c->trk[qi[i]].pinned,
-                               N * sizeof(int16_t), hipMemcpyHostToDevice, c->xfer));
+        HIP_TRY(hipMemcpyAsync(c->d_depth + (size_t)(d0 + i) * N,
+                               frames ? frames[i] : c->trk[qi[i]].pinned, N * sizeof(int16_t),
+                               hipMemcpyHostToDevice, c->xfer));
     HIP_TRY(hipEventRecord(ql.h2d, c->xfer));
     HIP_TRY(hipStreamWaitEvent(s, ql.h2d, 0));
     const int16_t* dsrc = c->d_depth + (size_t)d0 * N;
@@ -4026,10 +4030,11 @@ int youth_icp_track_submit(youth_icp_ctx* c, const int16_t* depth, const double*
     return track_submit_frames(c, depth, 1, T_init);
 }
 
-int youth_icp_track_submit_batch(youth_icp_ctx* c, const int16_t* depth, int n_frames)
+// youth_icp_track_submit_batch (depth: n_frames consecutive frames, staged)
+// and youth_icp_track_submit_pinned (frames: the caller's page-locked buffers).
+static int track_submit_many(youth_icp_ctx* c, const int16_t* depth,
+                             const int16_t* const* frames, int n_frames)
 {
-    if (!c || !depth || n_frames < 1 || n_frames > YOUTH_TRACK_MAX_BATCH)
-        return set_error(YOUTH_EINVAL, "track_submit_batch: bad arguments (%d frames)", n_frames);
     if (c->trk_n + n_frames > kTrackDepth)
         return set_error(YOUTH_EINVAL, "track_submit_batch: %d + %d frames in flight (max %d)",
                          c->trk_n, n_frames, kTrackDepth);
@@ -4040,7 +4045,7 @@ int youth_icp_track_submit_batch(youth_icp_ctx* c, const int16_t* depth, int n_f
     const size_t N = c->N;
     int done = 0;
     if (c->track_ref < 0) {  // no reference yet: the first frame is only prepped
-        rc = track_submit_frames(c, depth, 1, nullptr);
+        rc = track_submit_frames(c, depth, 1, nullptr, frames);
         if (rc) return rc;
         done = 1;
     }
@@ -4048,11 +4053,45 @@ int youth_icp_track_submit_batch(youth_icp_ctx* c, const int16_t* depth, int n_f
     while (done < n_frames) {
         int m = n_frames - done;
         while (m > 1 && !trk_chain_fits(c, m)) --m;
-        rc = track_submit_frames(c, depth + (size_t)done * N, m, nullptr);
+        rc = track_submit_frames(c, frames ? nullptr : depth + (size_t)done * N, m, nullptr,
+                                 frames ? frames + done : nullptr);
         if (rc) return rc;
+        if (m > 1) c->trk_chained_frames += m;
         done += m;
     }
     return YOUTH_OK;
+}
+
+int youth_icp_track_submit_batch(youth_icp_ctx* c, const int16_t* depth, int n_frames)
+{
+    if (!c || !depth || n_frames < 1 || n_frames > YOUTH_TRACK_MAX_BATCH)
+        return set_error(YOUTH_EINVAL, "track_submit_batch: bad arguments (%d frames)", n_frames);
+    return track_submit_many(c, depth, nullptr, n_frames);
+}
+
+int youth_icp_track_submit_pinned(youth_icp_ctx* c, const int16_t* const* frames, int n_frames)
+{
+    if (!c || !frames || n_frames < 1 || n_frames > YOUTH_TRACK_MAX_BATCH)
+        return set_error(YOUTH_EINVAL, "track_submit_pinned: bad arguments (%d frames)", n_frames);
+    for (int i = 0; i < n_frames; ++i)
+        if (!frames[i]) return set_error(YOUTH_EINVAL, "track_submit_pinned: frame %d is null", i);
+    return track_submit_many(c, nullptr, frames, n_frames);
+}
+
+int16_t* youth_icp_host_alloc(size_t values)
+{
+    if (!values) return nullptr;
+    int16_t* p = nullptr;
+    if (hipHostMalloc((void**)&p, values * sizeof(int16_t), hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return p;
+}
+
+void youth_icp_host_free(int16_t* p)
+{
+    if (p) (void)hipHostFree(p);
 }
 
 int youth_icp_track_collect(youth_icp_ctx* c, double* T_rel, int* has_ref)
@@ -4174,6 +4213,11 @@ int youth_icp_track_set_batch(youth_icp_ctx* c, int frames)
 }
 
 long long youth_icp_track_chained(const youth_icp_ctx* c) { return c ? c->trk_chained : 0; }
+
+long long youth_icp_track_chained_frames(const youth_icp_ctx* c)
+{
+    return c ? c->trk_chained_frames : 0;
+}
 
 void youth_icp_track_reset(youth_icp_ctx* c)
 {

@@ -32,16 +32,119 @@
 #include "youth_icp.h"
 
 // ------------------------------------------------------- ingest queue -----
+// Frames live in reusable buffers: a push copies the caller's frame into a
+// free buffer of the queue's pool (the one host copy of a frame on the SLAM
+// path), the drop policy and pops hand buffers back to the pool.  The SLAM
+// module's queue uses page-locked buffers (youth_icp_host_alloc, up to
+// kPinnedBytes of them), which the worker takes out of the queue and submits
+// to the tracker in place (youth_icp_track_submit_pinned), returning each to
+// the pool once its frame has been collected.
 struct youth_frame_queue {
     struct Item {
-        std::vector<int16_t> depth;
-        int w, h;
-        uint32_t ts;
+        int16_t* buf = nullptr;
+        size_t cap = 0;      // values the buffer holds
+        bool pinned = false;
+        int w = 0, h = 0;
+        uint32_t ts = 0;
     };
+    static constexpr size_t kPinnedBytes = (size_t)256 << 20;
+    static constexpr size_t kPoolMax = 48;  // free buffers kept
     std::mutex mu;
     std::deque<Item> q;
+    std::vector<Item> pool;
     int high = 10, low = 5;
+    bool pinned = false;      // allocate page-locked buffers (SLAM module queue)
+    size_t pinned_bytes = 0;  // page-locked bytes allocated and not freed
 };
+
+namespace {
+
+void buf_free(youth_frame_queue* q, youth_frame_queue::Item& it)
+{
+    if (!it.buf) return;
+    if (it.pinned) {
+        youth_icp_host_free(it.buf);
+        std::lock_guard<std::mutex> lk(q->mu);
+        q->pinned_bytes -= it.cap * sizeof(int16_t);
+    } else {
+        free(it.buf);
+    }
+    it.buf = nullptr;
+    it.cap = 0;
+}
+
+// a buffer of >= n values: from the pool, else newly allocated (page-locked
+// while the queue's budget lasts)
+bool buf_get(youth_frame_queue* q, size_t n, youth_frame_queue::Item& it)
+{
+    youth_frame_queue::Item old;
+    bool want_pinned = false;
+    {
+        std::lock_guard<std::mutex> lk(q->mu);
+        if (!q->pool.empty()) {
+            old = q->pool.back();
+            q->pool.pop_back();
+            if (old.cap >= n) {
+                it.buf = old.buf;
+                it.cap = old.cap;
+                it.pinned = old.pinned;
+                return true;
+            }
+        }
+        want_pinned = q->pinned && q->pinned_bytes + n * sizeof(int16_t) <= q->kPinnedBytes;
+        if (want_pinned) q->pinned_bytes += n * sizeof(int16_t);
+    }
+    buf_free(q, old);  // too small for this frame size
+    it.buf = want_pinned ? youth_icp_host_alloc(n) : nullptr;
+    it.pinned = it.buf != nullptr;
+    if (want_pinned && !it.buf) {
+        std::lock_guard<std::mutex> lk(q->mu);
+        q->pinned_bytes -= n * sizeof(int16_t);
+    }
+    if (!it.buf) it.buf = static_cast<int16_t*>(malloc(n * sizeof(int16_t)));
+    it.cap = it.buf ? n : 0;
+    return it.buf != nullptr;
+}
+
+// back to the pool (q->mu held), or freed when the pool is full
+void pool_put_locked(youth_frame_queue* q, youth_frame_queue::Item& it,
+                     std::vector<youth_frame_queue::Item>& to_free)
+{
+    if (!it.buf) return;
+    if (q->pool.size() < q->kPoolMax)
+        q->pool.push_back(it);
+    else
+        to_free.push_back(it);
+    it.buf = nullptr;
+}
+
+void free_all(youth_frame_queue* q, std::vector<youth_frame_queue::Item>& v)
+{
+    for (auto& it : v) buf_free(q, it);
+    v.clear();
+}
+
+// The oldest frame, buffer and all (1), or 0 when empty.
+int queue_take(youth_frame_queue* q, youth_frame_queue::Item& out)
+{
+    std::lock_guard<std::mutex> lk(q->mu);
+    if (q->q.empty()) return 0;
+    out = q->q.front();
+    q->q.pop_front();
+    return 1;
+}
+
+void queue_release(youth_frame_queue* q, youth_frame_queue::Item& it)
+{
+    std::vector<youth_frame_queue::Item> to_free;
+    {
+        std::lock_guard<std::mutex> lk(q->mu);
+        pool_put_locked(q, it, to_free);
+    }
+    free_all(q, to_free);
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -54,33 +157,45 @@ youth_frame_queue* youth_queue_create(int high_water, int low_water)
     return q;
 }
 
-void youth_queue_destroy(youth_frame_queue* q) { delete q; }
+void youth_queue_destroy(youth_frame_queue* q)
+{
+    if (!q) return;
+    std::vector<youth_frame_queue::Item> all(q->q.begin(), q->q.end());
+    all.insert(all.end(), q->pool.begin(), q->pool.end());
+    q->q.clear();
+    q->pool.clear();
+    free_all(q, all);
+    delete q;
+}
 
 int youth_queue_push(youth_frame_queue* q, const int16_t* depth, int width, int height,
                      uint32_t timestamp)
 {
     if (!q || !depth || width <= 0 || height <= 0) return YOUTH_EINVAL;
+    const size_t n = (size_t)width * (size_t)height;
     youth_frame_queue::Item it;
-    try {
-        it.depth.assign(depth, depth + (size_t)width * (size_t)height);
-    } catch (...) {
-        return YOUTH_ENOMEM;
-    }
+    if (!buf_get(q, n, it)) return YOUTH_ENOMEM;
+    memcpy(it.buf, depth, n * sizeof(int16_t));
     it.w = width;
     it.h = height;
     it.ts = timestamp;
-    std::lock_guard<std::mutex> lk(q->mu);
-    q->q.push_back(std::move(it));
+    std::vector<youth_frame_queue::Item> to_free;
     int dropped = 0;
-    // SLAM.cpp:163-168: size > 10 -> pop the oldest down to 5
-    if ((int)q->q.size() > q->high) {
-        fprintf(stderr, "youth_icp: frame queue is getting large (%zu), dropping to %d\n",
-                q->q.size(), q->low);
-        while ((int)q->q.size() > q->low) {
-            q->q.pop_front();
-            ++dropped;
+    {
+        std::lock_guard<std::mutex> lk(q->mu);
+        q->q.push_back(it);
+        // SLAM.cpp:163-168: size > 10 -> pop the oldest down to 5
+        if ((int)q->q.size() > q->high) {
+            fprintf(stderr, "youth_icp: frame queue is getting large (%zu), dropping to %d\n",
+                    q->q.size(), q->low);
+            while ((int)q->q.size() > q->low) {
+                pool_put_locked(q, q->q.front(), to_free);
+                q->q.pop_front();
+                ++dropped;
+            }
         }
     }
+    free_all(q, to_free);
     return dropped;
 }
 
@@ -88,15 +203,20 @@ int youth_queue_pop(youth_frame_queue* q, int16_t* depth_out, size_t cap, int* w
                     int* height, uint32_t* timestamp)
 {
     if (!q) return YOUTH_EINVAL;
-    std::lock_guard<std::mutex> lk(q->mu);
-    if (q->q.empty()) return 0;
-    auto& it = q->q.front();
-    if (it.depth.size() > cap || !depth_out) return YOUTH_EINVAL;
-    memcpy(depth_out, it.depth.data(), it.depth.size() * sizeof(int16_t));
+    youth_frame_queue::Item it;
+    {
+        std::lock_guard<std::mutex> lk(q->mu);
+        if (q->q.empty()) return 0;
+        const auto& f = q->q.front();
+        if ((size_t)f.w * (size_t)f.h > cap || !depth_out) return YOUTH_EINVAL;
+        it = f;
+        q->q.pop_front();
+    }
+    memcpy(depth_out, it.buf, (size_t)it.w * it.h * sizeof(int16_t));
     if (width) *width = it.w;
     if (height) *height = it.h;
     if (timestamp) *timestamp = it.ts;
-    q->q.pop_front();
+    queue_release(q, it);
     return 1;
 }
 
@@ -110,8 +230,13 @@ int youth_queue_size(youth_frame_queue* q)
 void youth_queue_clear(youth_frame_queue* q)
 {
     if (!q) return;
-    std::lock_guard<std::mutex> lk(q->mu);
-    q->q.clear();
+    std::vector<youth_frame_queue::Item> to_free;
+    {
+        std::lock_guard<std::mutex> lk(q->mu);
+        for (auto& it : q->q) pool_put_locked(q, it, to_free);
+        q->q.clear();
+    }
+    free_all(q, to_free);
 }
 
 // ---------------------------------------------------------- YAML config ---
@@ -196,46 +321,45 @@ youth_intrinsics intrinsics_for(int w, int h)
 }
 
 // SLAM.cpp:32-63 processFramesThread, with TrackRGBD replaced by HIP ICP.
-// Pipelined two deep (youth_icp_track_submit / _collect): after submitting
-// frame k the worker collects frame k-1, so frame k's upload and align run
-// while the host records k-1's pose and pops k+1.  A frame's pose reaches
-// the trajectory when the next frame is submitted or the queue runs empty
-// (the worker stays busy until then: youth_slam_wait_idle).
-// YOUTH_SLAM_TRACK_BATCH=m, 2 <= m <= YOUTH_TRACK_MAX_BATCH (opt-in, for
-// backlogged queues such as a .bin replay): frames of the same size already
-// queued behind the popped one (up to m in all) are tracked as one
-// micro-batch (youth_icp_track_submit_batch), two submissions in flight;
-// every frame then runs on the batch plan, so a pose
-// does not depend on whether its frame was batched.
+// The worker takes every frame of the current size already queued behind
+// the one it pops, up to `batch` (YOUTH_TRACK_MAX_BATCH by default;
+// YOUTH_SLAM_TRACK_BATCH=m overrides, 1 = one frame per launch), and
+// submits them as ONE micro-batch (youth_icp_track_submit_pinned: the queue's
+// page-locked buffers are copied to the device in place), two submissions in
+// flight.  The context is planned for `batch` (youth_icp_track_set_batch), so
+// every frame runs on that plan whether it arrived alone (a live camera) or
+// in a backlog (a .bin replay, a burst): a frame's pose does not depend on
+// the queue's timing.  A frame's pose reaches the trajectory when the
+// submission after its own is made or the queue runs empty (the worker stays
+// busy until then: youth_slam_wait_idle).
 void worker_main(int device)
 {
+    using Item = youth_frame_queue::Item;
     fprintf(stderr, "youth_icp: SLAM processing thread started\n");
     youth_icp_ctx* ctx = nullptr;
     int cw = 0, ch = 0;
     const char* eb = getenv("YOUTH_SLAM_TRACK_BATCH");
-    const int batch = eb ? std::max(1, std::min(atoi(eb), YOUTH_TRACK_MAX_BATCH)) : 1;
-    const size_t kMaxFrame = (size_t)4096 * 4096;
-    std::vector<int16_t> buf;
-    // one kMaxFrame buffer: the popped frame at 0, a micro-batch's further
-    // frames at m N, and past them the pop target for the next one
-    bool held = false;  // a popped frame not yet submitted, at buf[held_off]
-    size_t held_off = 0;
-    int held_w = 0, held_h = 0;
-    uint32_t held_ts = 0;
+    const int batch = eb ? std::max(1, std::min(atoi(eb), YOUTH_TRACK_MAX_BATCH))
+                         : YOUTH_TRACK_MAX_BATCH;
+    std::vector<int16_t> packed;  // pageable frames of a micro-batch, packed (rare)
+    bool held = false;            // a taken frame of another size (or sequence), next round
+    Item held_item;
     double T_w_ref[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
     struct Pending {
         uint32_t ts;
-        int npts;
+        int npts;   // valid pixels (counted for the last frame of a submission, else -1)
+        Item item;  // its buffer, in use by the H2D until the frame is collected
     };
     std::deque<Pending> pend;  // submitted, not yet collected (oldest first)
     // collect the oldest submitted frame; record its pose unless a reset
-    // arrived since it was submitted
+    // arrived since it was submitted; its buffer goes back to the pool
     auto finish_one = [&](bool record) {
-        const Pending pr0 = pend.front();
+        Pending pr0 = pend.front();
         pend.pop_front();
         double T_rel[16];
         int has_ref = 0;
         const int st = youth_icp_track_collect(ctx, T_rel, &has_ref);
+        queue_release(g_queue, pr0.item);
         if (st < 0) {
             fprintf(stderr, "youth_icp: tracking failed: %s\n", youth_icp_last_error());
             return;
@@ -259,22 +383,17 @@ void worker_main(int device)
         pr.ts = pr0.ts;
         memcpy(pr.T, T_w_ref, sizeof(pr.T));
         g_traj.push_back(pr);
-        g_last_points = pr0.npts;
+        if (pr0.npts >= 0) g_last_points = pr0.npts;
     };
     while (g_process.load()) {
-        if (buf.empty()) buf.resize(kMaxFrame);
-        int w = 0, h = 0;
-        uint32_t ts = 0;
+        Item items[YOUTH_TRACK_MAX_BATCH];
         g_busy.store(true);
         int got = 1;
         if (held) {
-            memmove(buf.data(), buf.data() + held_off, (size_t)held_w * held_h * sizeof(int16_t));
-            w = held_w;
-            h = held_h;
-            ts = held_ts;
+            items[0] = held_item;
             held = false;
         } else {
-            got = youth_queue_pop(g_queue, buf.data(), kMaxFrame, &w, &h, &ts);
+            got = queue_take(g_queue, items[0]);
         }
         if (got != 1) {
             if (!pend.empty()) {  // nothing new: finish what is in flight
@@ -282,9 +401,10 @@ void worker_main(int device)
                 continue;
             }
             g_busy.store(false);
-            std::this_thread::sleep_for(std::chrono::milliseconds(got == 0 ? 1 : 5));
+            std::this_thread::sleep_for(std::chrono::milliseconds(1));
             continue;
         }
+        const int w = items[0].w, h = items[0].h;
         if (g_reset.exchange(false)) {
             while (!pend.empty()) finish_one(false);  // frames of the old sequence
             if (ctx) youth_icp_track_reset(ctx);
@@ -300,61 +420,64 @@ void worker_main(int device)
                 fprintf(stderr, "youth_icp: context creation failed: %s\n",
                         youth_icp_last_error());
                 cw = ch = 0;
+                queue_release(g_queue, items[0]);
                 g_busy.store(false);
                 continue;
             }
             if (batch > 1) youth_icp_track_set_batch(ctx, batch);
         }
         const size_t N = (size_t)w * h;
-        auto count_points = [&](const int16_t* d) {
-            int n = 0;
-            for (size_t i = 0; i < N; ++i) n += d[i] > 0;
-            return n;
-        };
-        // micro-batch: frames of this size already waiting, up to `batch`
-        // in all (one of another size, or of a sequence reset since, is held
-        // for the next round)
+        // the micro-batch: frames of this size already waiting, up to `batch`
+        // in all (one of another size, or taken after a reset, is held for
+        // the next round)
         int m = 1;
-        uint32_t tss[YOUTH_TRACK_MAX_BATCH] = {};
-        tss[0] = ts;
-        const int mmax = (int)std::max<size_t>(1, std::min<size_t>(batch, kMaxFrame / N - 1));
-        int16_t* const scratch = buf.data() + (size_t)mmax * N;  // >= N values left
-        while (m < mmax && !held && youth_queue_size(g_queue) > 0) {
-            int w2 = 0, h2 = 0;
-            uint32_t t2 = 0;
-            // a larger frame does not fit and stays queued for the next round
-            if (youth_queue_pop(g_queue, scratch, kMaxFrame - (size_t)mmax * N, &w2, &h2, &t2) != 1)
-                break;
-            if (w2 == w && h2 == h && !g_reset.load()) {
-                memmove(buf.data() + m * N, scratch, N * sizeof(int16_t));
-                tss[m++] = t2;
+        while (m < batch && !held) {
+            Item it;
+            if (queue_take(g_queue, it) != 1) break;
+            if (it.w == w && it.h == h && !g_reset.load()) {
+                items[m++] = it;
             } else {
+                held_item = it;
                 held = true;
-                held_off = (size_t)mmax * N;
-                held_w = w2;
-                held_h = h2;
-                held_ts = t2;
             }
         }
         // two submissions in flight: frames, or micro-batches
         while (!pend.empty() && (int)pend.size() + m > 2 * batch) finish_one(true);
-        const long long chained0 = youth_icp_track_chained(ctx);
-        const int rc = m == 1 ? youth_icp_track_submit(ctx, buf.data(), nullptr)
-                              : youth_icp_track_submit_batch(ctx, buf.data(), m);
-        // frames of a micro-batch that ran chained
-        if (youth_icp_track_chained(ctx) > chained0) g_batched.fetch_add(m);
-        if (rc < 0) {
-            fprintf(stderr, "youth_icp: tracking failed: %s\n", youth_icp_last_error());
-            // a micro-batch may have submitted its first frames before failing
-            const int sent = youth_icp_track_pending(ctx) - (int)pend.size();
-            for (int i = 0; i < sent && i < m; ++i)
-                pend.push_back(Pending{tss[i], count_points(buf.data() + i * N)});
-            continue;
+        const long long chained0 = youth_icp_track_chained_frames(ctx);
+        bool pinned = true;
+        for (int i = 0; i < m; ++i) pinned &= items[i].pinned;
+        int rc;
+        if (pinned) {
+            const int16_t* fr[YOUTH_TRACK_MAX_BATCH];
+            for (int i = 0; i < m; ++i) fr[i] = items[i].buf;
+            rc = youth_icp_track_submit_pinned(ctx, fr, m);
+        } else if (m == 1) {
+            rc = youth_icp_track_submit(ctx, items[0].buf, nullptr);
+        } else {
+            packed.resize((size_t)m * N);
+            for (int i = 0; i < m; ++i)
+                memcpy(packed.data() + (size_t)i * N, items[i].buf, N * sizeof(int16_t));
+            rc = youth_icp_track_submit_batch(ctx, packed.data(), m);
         }
-        for (int i = 0; i < m; ++i) pend.push_back(Pending{tss[i], count_points(buf.data() + i * N)});
+        // frames of this submission that ran in chained (micro-batch) launches
+        g_batched.fetch_add(youth_icp_track_chained_frames(ctx) - chained0);
+        // getSlamMapPoints reports the newest recorded frame: only the last
+        // frame of a submission is counted
+        int npts = 0;
+        for (size_t i = 0; i < N; ++i) npts += items[m - 1].buf[i] > 0;
+        // a failed micro-batch may have submitted its first frames
+        const int sent = rc < 0 ? youth_icp_track_pending(ctx) - (int)pend.size() : m;
+        if (rc < 0) fprintf(stderr, "youth_icp: tracking failed: %s\n", youth_icp_last_error());
+        for (int i = 0; i < m; ++i) {
+            if (i < sent)
+                pend.push_back(Pending{items[i].ts, i == m - 1 ? npts : -1, items[i]});
+            else
+                queue_release(g_queue, items[i]);
+        }
         if (batch == 1 && pend.size() == 2) finish_one(true);
     }
     while (ctx && !pend.empty()) finish_one(true);
+    if (held) queue_release(g_queue, held_item);
     if (ctx) youth_icp_destroy(ctx);
     fprintf(stderr, "youth_icp: SLAM processing thread stopped\n");
 }
@@ -450,7 +573,10 @@ void initSlamModule(const char* config_file, const char* vocabulary_file)
     int device = 0;
     if (const char* e = getenv("YOUTH_ICP_DEVICE")) device = atoi(e);
     if (device < 0 || device >= ndev) device = 0;
-    if (!g_queue) g_queue = youth_queue_create(10, 5);
+    if (!g_queue) {
+        g_queue = youth_queue_create(10, 5);
+        g_queue->pinned = true;  // buffers the tracker copies to the device in place
+    }
     youth_queue_clear(g_queue);
     g_traj.clear();
     g_last_points = 0;
@@ -581,6 +707,8 @@ int youth_slam_get_pose(int index, uint32_t* timestamp, double* T_wc)
 }
 
 long long youth_slam_batched_frames(void) { return g_batched.load(); }
+
+int youth_slam_queue_size(void) { return g_queue ? youth_queue_size(g_queue) : 0; }
 
 int youth_slam_wait_idle(int timeout_ms)
 {

@@ -145,6 +145,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "youth_icp_track_submit_batch": (c_int, [c_void_p, P16, c_int]),
         "youth_icp_track_set_batch": (c_int, [c_void_p, c_int]),
         "youth_icp_track_chained": (ctypes.c_longlong, [c_void_p]),
+        "youth_icp_track_chained_frames": (ctypes.c_longlong, [c_void_p]),
+        "youth_icp_track_submit_pinned": (c_int, [c_void_p, POINTER(P16), c_int]),
+        "youth_icp_host_alloc": (P16, [c_size_t]),
+        "youth_icp_host_free": (None, [P16]),
         "youth_icp_track_host_sequence": (c_int, [c_void_p, P16, c_int, PD, POINTER(c_int32)]),
         "youth_parse_camera_yaml": (c_int, [c_char_p, POINTER(Intrinsics), POINTER(c_int),
                                             POINTER(c_int)]),
@@ -159,6 +163,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "youth_slam_get_trajectory": (c_int, [c_int, POINTER(c_uint32), PD]),
         "youth_slam_wait_idle": (c_int, [c_int]),
         "youth_slam_batched_frames": (ctypes.c_longlong, []),
+        "youth_slam_queue_size": (c_int, []),
         "youth_slam_wait_stopped": (None, []),
     }
     ab_build = bool(os.environ.get("YOUTH_ICP_LIB"))  # tools/ab_*.sh: older builds
@@ -260,8 +265,13 @@ def slam_wait_idle(timeout_ms: int = 10000) -> int:
 
 
 def slam_batched_frames() -> int:
-    """Frames the SLAM worker tracked in micro-batches (YOUTH_SLAM_TRACK_BATCH=2)."""
+    """Frames the SLAM worker aligned in chained micro-batch launches."""
     return int(load_library().youth_slam_batched_frames())
+
+
+def slam_queue_size() -> int:
+    """Frames waiting in the SLAM module's ingest queue."""
+    return load_library().youth_slam_queue_size()
 
 
 def slam_trajectory() -> tuple[np.ndarray, np.ndarray]:
@@ -317,6 +327,25 @@ class FrameQueue:
         if self._q:
             self._lib.youth_queue_destroy(self._q)
             self._q = None
+
+    __del__ = close
+
+
+class PinnedFrame:
+    """One page-locked host frame (youth_icp_host_alloc) as a numpy view."""
+
+    def __init__(self, height: int, width: int):
+        self._lib = load_library()
+        self.ptr = self._lib.youth_icp_host_alloc(width * height)
+        if not self.ptr:
+            raise IcpError(YOUTH_ENOMEM, "youth_icp_host_alloc failed")
+        self.array = np.ctypeslib.as_array(self.ptr, shape=(height, width))
+
+    def close(self):
+        if getattr(self, "ptr", None):
+            self.array = None
+            self._lib.youth_icp_host_free(self.ptr)
+            self.ptr = None
 
     __del__ = close
 
@@ -546,6 +575,16 @@ class IcpContext:
     def track_chained(self) -> int:
         """Micro-batch launches run so far on this context."""
         return int(self._lib.youth_icp_track_chained(self._ctx))
+
+    def track_chained_frames(self) -> int:
+        """Frames those micro-batch launches aligned."""
+        return int(self._lib.youth_icp_track_chained_frames(self._ctx))
+
+    def track_submit_pinned(self, frames) -> None:
+        """Submit PinnedFrames rows (or a list of them) without a staging copy
+        (youth_icp_track_submit_pinned); keep them unchanged until collected."""
+        ptrs = (POINTER(c_int16) * len(frames))(*[f.ptr for f in frames])
+        _check(self._lib.youth_icp_track_submit_pinned(self._ctx, ptrs, len(frames)))
 
     def track_pending(self) -> int:
         return int(self._lib.youth_icp_track_pending(self._ctx))

@@ -551,14 +551,20 @@ def test_slam_api_end_to_end():
     assert youth_icp.processSlamFrame(frames[0], None, 640, 480, 0) == 0
 
 
-@pytest.mark.parametrize("batch", [2, 8])
+@pytest.mark.parametrize("batch", [None, 2, 8])
 def test_slam_worker_micro_batches(monkeypatch, batch):
-    """YOUTH_SLAM_TRACK_BATCH=m: a backlogged queue (9 frames pushed at once,
-    under the reference's drop threshold of 10) is tracked in micro-batches
-    of up to m.  Every pose is the one the batch plan gives frame by frame
-    (composition aside: world poses within 1e-12 of the prefix product of
-    the context's relative poses) and within 1e-5 of the oracle's."""
-    monkeypatch.setenv("YOUTH_SLAM_TRACK_BATCH", str(batch))
+    """A backlogged queue (9 frames pushed at once, under the reference's
+    drop threshold of 10) is tracked in micro-batches of up to m frames: by
+    default (batch None: m = YOUTH_TRACK_MAX_BATCH, the queue's page-locked
+    buffers submitted in place) and with YOUTH_SLAM_TRACK_BATCH=m.  Every
+    pose is the one the batch plan gives frame by frame (composition aside:
+    world poses within 1e-12 of the prefix product of the context's relative
+    poses) and within 1e-5 of the oracle's."""
+    if batch is None:
+        monkeypatch.delenv("YOUTH_SLAM_TRACK_BATCH", raising=False)
+        batch = youth_icp.TRACK_MAX_BATCH
+    else:
+        monkeypatch.setenv("YOUTH_SLAM_TRACK_BATCH", str(batch))
     F = 9
     frames, _ = youth_synth.sequence(0, F)
     youth_icp.initSlamModule(os.path.join(GOLDEN, "astra_camera.yaml"), "ORBvoc.txt")

@@ -85,8 +85,13 @@ static void scenario_init_and_producers()
         check(youth_slam_batched_frames() > 0, "worker tracked micro-batches");
     done.store(true);
     reader.join();
+    // one more frame after the reader's reset (which may have come after the
+    // last producer frame was tracked): the trajectory is not empty
+    auto last = frame(4242);
+    check(processSlamFrame(last.data(), nullptr, W, H, 99999) == 1, "processSlamFrame accepted");
+    check(youth_slam_wait_idle(20000) == 1, "worker idle");
     const int len = youth_slam_trajectory_length();
-    check(len > 0 && len <= 160, "trajectory length bounded by frames pushed");
+    check(len > 0 && len <= 161, "trajectory length bounded by frames pushed");
     unlink((base + "_trajectory.txt").c_str());
     unlink((base + "_keyframes.txt").c_str());
 }

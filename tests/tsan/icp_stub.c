@@ -3,7 +3,8 @@
  * libyouth_icp device entry points the host-side threading code calls
  * (slam_api.cpp's worker: create / destroy / track_submit / track_collect /
  * track_frame / track_reset / track_submit_batch / track_set_batch /
- * track_chained / device_count / last_error, plus
+ * track_chained / track_chained_frames / track_submit_pinned /
+ * host_alloc / host_free / device_count / last_error, plus
  * youth_default_intrinsics), so the SLAM.h
  * queue + worker, the AlgorithmModule frame loop and the POSIX-queue
  * transport can run under ThreadSanitizer / AddressSanitizer on a machine
@@ -25,8 +26,27 @@ struct youth_icp_ctx {
     /* submitted frames' results, oldest first */
     double T[YOUTH_TRACK_MAX_IN_FLIGHT][16];
     int has[YOUTH_TRACK_MAX_IN_FLIGHT], n, head, batch;
-    long long chained;
+    long long chained, chained_frames;
+    /* in-place (pinned) submissions: the caller's buffer and its depth sum at
+     * submit time, re-read at collect (a buffer reused while its frame is in
+     * flight fails the run) */
+    const int16_t* src[YOUTH_TRACK_MAX_IN_FLIGHT];
+    long long src_sum[YOUTH_TRACK_MAX_IN_FLIGHT];
 };
+
+static long long depth_sum(const youth_icp_ctx* c, const int16_t* d)
+{
+    long long s = 0;
+    for (int i = 0; i < c->W * c->H; ++i) s += d[i];
+    return s;
+}
+
+int16_t* youth_icp_host_alloc(size_t values)
+{
+    return values ? (int16_t*)malloc(values * sizeof(int16_t)) : NULL;
+}
+
+void youth_icp_host_free(int16_t* p) { free(p); }
 
 int youth_icp_device_count(void) { return 1; }
 const char* youth_icp_last_error(void) { return "stub"; }
@@ -57,6 +77,7 @@ int youth_icp_track_submit(youth_icp_ctx* c, const int16_t* depth, const double*
     if (c->n >= YOUTH_TRACK_MAX_IN_FLIGHT) return YOUTH_EINVAL;
     const int j = (c->head + c->n) % YOUTH_TRACK_MAX_IN_FLIGHT;
     stub_track(c, depth, c->T[j], &c->has[j]);
+    c->src[j] = NULL;
     ++c->n;
     return 0;
 }
@@ -66,6 +87,7 @@ int youth_icp_track_collect(youth_icp_ctx* c, double* T_rel, int* has_ref)
     if (c->n == 0) return YOUTH_EINVAL;
     struct timespec ts = {0, 200 * 1000}; /* a GPU align takes ~100 us */
     nanosleep(&ts, NULL);
+    if (c->src[c->head] && depth_sum(c, c->src[c->head]) != c->src_sum[c->head]) abort();
     memcpy(T_rel, c->T[c->head], 16 * sizeof(double));
     if (has_ref) *has_ref = c->has[c->head];
     c->head = (c->head + 1) % YOUTH_TRACK_MAX_IN_FLIGHT;
@@ -83,6 +105,7 @@ int youth_icp_track_set_batch(youth_icp_ctx* c, int frames)
 }
 
 long long youth_icp_track_chained(const youth_icp_ctx* c) { return c->chained; }
+long long youth_icp_track_chained_frames(const youth_icp_ctx* c) { return c->chained_frames; }
 
 /* as the library: a sequence's first frame alone, then one "launch" */
 int youth_icp_track_submit_batch(youth_icp_ctx* c, const int16_t* depth, int n_frames)
@@ -90,10 +113,30 @@ int youth_icp_track_submit_batch(youth_icp_ctx* c, const int16_t* depth, int n_f
     if (n_frames < 1 || n_frames > YOUTH_TRACK_MAX_BATCH ||
         c->n + n_frames > YOUTH_TRACK_MAX_IN_FLIGHT)
         return YOUTH_EINVAL;
-    const int chain = c->has_ref && n_frames > 1;
+    const int first_alone = !c->has_ref;
+    const int chain = n_frames - first_alone > 1;
     for (int i = 0; i < n_frames; ++i)
         youth_icp_track_submit(c, depth + (size_t)i * c->W * c->H, NULL);
     c->chained += chain;
+    c->chained_frames += chain ? n_frames - first_alone : 0;
+    return 0;
+}
+
+int youth_icp_track_submit_pinned(youth_icp_ctx* c, const int16_t* const* frames, int n_frames)
+{
+    if (n_frames < 1 || n_frames > YOUTH_TRACK_MAX_BATCH ||
+        c->n + n_frames > YOUTH_TRACK_MAX_IN_FLIGHT)
+        return YOUTH_EINVAL;
+    const int first_alone = !c->has_ref;
+    const int chain = n_frames - first_alone > 1;
+    for (int i = 0; i < n_frames; ++i) {
+        const int j = (c->head + c->n) % YOUTH_TRACK_MAX_IN_FLIGHT;
+        youth_icp_track_submit(c, frames[i], NULL);
+        c->src[j] = frames[i];
+        c->src_sum[j] = depth_sum(c, frames[i]);
+    }
+    c->chained += chain;
+    c->chained_frames += chain ? n_frames - first_alone : 0;
     return 0;
 }
 
