@@ -76,16 +76,26 @@ def test_bench_single_gpu_contract():
     assert all(v > 0 for v in d["c5"]["streamed"]["batched_launches"].values())
     assert d["kernel_path"]["kernel"].startswith("k_prep + k_icp")
     assert d["viewer_cloud"]["bit_exact_vs_cpu"]
-    # spec a7/a8: the default is SURVEY §8a as worded; both arithmetics
-    # against the survey-spec oracle and their own
-    assert d["spec"]["name"] == "survey"
+    # spec a7/a8: the default is SURVEY §8a as worded; a9: fp32 lanes -> fp64
+    # finalize (SURVEY §8a a9 as worded).  Every arithmetic x reduction against
+    # the survey-spec exact oracle (<= 1e-5) and against the oracle in the
+    # same variant (lane32 over the launch's own lane partition: ~1e-13)
+    assert d["spec"]["name"] == "survey" and d["spec"]["a9_reduce"] == "lane32"
     sp = d["spec_parity"]
+    assert sp["default_variant"] == "survey_lane32"
     for case in ("c2_64_pairs", "c3_2_pairs_1280x960_20it", "c5_200_pairs",
                  "survey_noise_16_pairs"):
-        assert sp[case]["gpu_survey_vs_survey_oracle"] <= 1e-5, case
-        assert sp[case]["gpu_fma_vs_fma_oracle"] <= 1e-5, case
+        for v in ("survey", "fma", "survey_lane32", "fma_lane32"):
+            assert sp[case][f"gpu_{v}_vs_same_variant_oracle"] <= 1e-9, (case, v)
+        for v in ("survey", "survey_lane32"):
+            assert sp[case][f"gpu_{v}_vs_survey_oracle"] <= 1e-5, (case, v)
     assert sp["default_within_tol_of_survey_spec"]
     assert sp["other_spec_rate"]["spec"] == "fma" and sp["other_spec_rate"]["value"] > 0
+    assert sp["other_reduce_rate"]["reduce"] == "exact" and sp["other_reduce_rate"]["value"] > 0
+    sa = d["c5"]["streamed"]["slam_api"]          # processSlamFrame, worker micro-batches
+    assert sa["value"] > 0 and sa["frames_recorded"] == sa["frames"] and sa["timestamps_in_order"]
+    assert sa["world_pose_max_abs_diff_vs_track_frame_plan"] <= 1e-12
+    assert sum(sa["batched_frames_per_pass"]) > 0
     assert d["ranks"]["rccl_world_size"] == 1 and d["ranks"]["per_rank_ms"]["k_icp_ms"][0] > 0
 
 
