@@ -62,14 +62,22 @@ constexpr int kTileW = 64;
 // 64 x 48 / 512 593 us, 64 x 80 and 64 x 96 by 1024 threads 625-643 us
 // (profiles/r02/ab_s44.txt, ab_s45.txt); fewer workgroups per CU cost more
 // (ab_s43.txt: 7 -> 6 per CU +8 %)
-constexpr int kTileH = 48;
 constexpr int kPrepThreads = 512;
+// k_prep's own tile (A/B knobs; k_icp_coop's fused prep keeps kTileW-wide
+// tiles, whose shape its lane partition and prep counters assume)
+#ifndef YOUTH_PREP_TW
+#define YOUTH_PREP_TW 64
+#endif
+#ifndef YOUTH_PREP_TH
+#define YOUTH_PREP_TH 48
+#endif
+constexpr int kPrepTW = YOUTH_PREP_TW;
+constexpr int kPrepTH = YOUTH_PREP_TH;
 // frames in flight through youth_icp_track_submit (YOUTH_TRACK_MAX_IN_FLIGHT):
 // two one at a time, or two micro-batches of two, so the next submission's
 // host copy and H2D overlap the launch before it
 constexpr int kTrackDepth = YOUTH_TRACK_MAX_IN_FLIGHT;
 constexpr int kLdsW = kTileW + 2;
-constexpr int kLdsH = kTileH + 2;
 
 constexpr int kRedThreads = 256;
 constexpr int kRedStep = kRedThreads * 4;  // pixels per workgroup loop step
@@ -518,20 +526,22 @@ __global__ void k_selftest_normalize(unsigned long long n, unsigned long long se
 // buffer stores) for an in-launch hand-off (k_icp_coop).  Contains a
 // workgroup barrier (every thread must call it); a caller reusing the LDS
 // planes for another tile adds one more before it.
-template <bool kFast, bool kWide, bool kSc1, int kThreads, int kTH>
+template <bool kFast, bool kWide, bool kSc1, int kThreads, int kTH, int kTW = kTileW>
 __device__ __forceinline__ void prep_tile(const int16_t* __restrict__ dep, float4* __restrict__ R,
                                           int W, int H, size_t P, const Intr& K, const FastK& F,
                                           float* __restrict__ X, int x0, int y0, float* sX,
                                           float* sY, float* sZ)
 {
     constexpr int kLH = kTH + 2;
-    const int tx = threadIdx.x & 63;
-    const int ty = threadIdx.x >> 6;
+    constexpr int kLW = kTW + 2;
+    static_assert(kTW % 64 == 0 && kThreads % kTW == 0, "rows of whole waves");
+    const int tx = threadIdx.x % kTW;
+    const int ty = threadIdx.x / kTW;
     if (kWide) {
         // W % 4 == 0 (and an 8-byte-aligned frame): columns [x0-4, x0+68) as
         // 18 aligned 8-byte words per halo row; each word's 4 pixels are all
         // inside or all outside the image, so no lane straddles an edge.
-        constexpr int kWords = (kTileW + 8) / 4;  // 18
+        constexpr int kWords = (kTW + 8) / 4;  // 18 at 64
         for (int e = threadIdx.x; e < kLH * kWords; e += kThreads) {
             const int ly = e / kWords;
             const int m = e - ly * kWords;
@@ -544,25 +554,25 @@ __device__ __forceinline__ void prep_tile(const int16_t* __restrict__ dep, float
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int lx = 4 * m - 3 + q;  // LDS column of pixel c + q
-                if (lx < 0 || lx >= kLdsW) continue;
+                if (lx < 0 || lx >= kLW) continue;
                 float x, y, z;
                 backproject<kFast>(dv[q], c + q, gy, K, F, x, y, z);
-                sX[ly * kLdsW + lx] = x;
-                sY[ly * kLdsW + lx] = y;
-                sZ[ly * kLdsW + lx] = z;
+                sX[ly * kLW + lx] = x;
+                sY[ly * kLW + lx] = y;
+                sZ[ly * kLW + lx] = z;
             }
         }
     } else {
-        for (int e = threadIdx.x; e < kLH * kLdsW; e += kThreads) {
-            const int ly = e / kLdsW;
-            const int lx = e - ly * kLdsW;
+        for (int e = threadIdx.x; e < kLH * kLW; e += kThreads) {
+            const int ly = e / kLW;
+            const int lx = e - ly * kLW;
             const int gx = x0 - 1 + lx, gy = y0 - 1 + ly;
             float x = 0.0f, y = 0.0f, z = 0.0f;
             if (gx >= 0 && gx < W && gy >= 0 && gy < H)
                 backproject<kFast>(dep[(size_t)gy * W + gx], gx, gy, K, F, x, y, z);
-            sX[ly * kLdsW + lx] = x;
-            sY[ly * kLdsW + lx] = y;
-            sZ[ly * kLdsW + lx] = z;
+            sX[ly * kLW + lx] = x;
+            sY[ly * kLW + lx] = y;
+            sZ[ly * kLW + lx] = z;
         }
     }
     __syncthreads();
@@ -573,13 +583,13 @@ __device__ __forceinline__ void prep_tile(const int16_t* __restrict__ dep, float
     // offsets stay on the scalar unit
     const int tyw = __builtin_amdgcn_readfirstlane(ty);
 #pragma unroll
-    for (int k = 0; k < kTH / (kThreads / 64); ++k) {
-        const int row = tyw + (kThreads / 64) * k;
+    for (int k = 0; k < kTH / (kThreads / kTW); ++k) {
+        const int row = tyw + (kThreads / kTW) * k;
         const int gx = x0 + tx, gy = y0 + row;
         if (gx >= W || gy >= H) continue;
         const size_t i = (size_t)gy * W + gx;
         const int ly = row + 1, lx = tx + 1;
-        const int o = ly * kLdsW + lx;
+        const int o = ly * kLW + lx;
         const float px = sX[o], py = sY[o], pz = sZ[o];
         if (X) {
             X[i] = px;
@@ -594,15 +604,15 @@ __device__ __forceinline__ void prep_tile(const int16_t* __restrict__ dep, float
         // non-negative floats; +0 is bits 0)
         const bool inner = (gx > 0) & (gy > 0) & (gx < W - 1) & (gy < H - 1);
         const float zl = sZ[o - 1], zr = sZ[o + 1];
-        const float zu = sZ[o - kLdsW], zd = sZ[o + kLdsW];
+        const float zu = sZ[o - kLW], zd = sZ[o + kLW];
         const unsigned zmin = min(min(min(__float_as_uint(pz), __float_as_uint(zl)),
                                       min(__float_as_uint(zr), __float_as_uint(zu))),
                                   __float_as_uint(zd));
         const float ax = sX[o + 1] - sX[o - 1];
         const float ay = sY[o + 1] - sY[o - 1];
         const float az = zr - zl;
-        const float bx = sX[o + kLdsW] - sX[o - kLdsW];
-        const float by = sY[o + kLdsW] - sY[o - kLdsW];
+        const float bx = sX[o + kLW] - sX[o - kLW];
+        const float by = sY[o + kLW] - sY[o - kLW];
         const float bz = zd - zu;
         const float cx = ay * bz - az * by;
         const float cy = az * bx - ax * bz;
@@ -733,13 +743,13 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const int16_t* __restrict
     const int ty = r / tiles_x;
     const int tx = r - ty * tiles_x;
     init_pairs(ia, tx, ty, f, n_frames);
-    __shared__ float sX[kLdsH * kLdsW];
-    __shared__ float sY[kLdsH * kLdsW];
-    __shared__ float sZ[kLdsH * kLdsW];
+    __shared__ float sX[(kPrepTH + 2) * (kPrepTW + 2)];
+    __shared__ float sY[(kPrepTH + 2) * (kPrepTW + 2)];
+    __shared__ float sZ[(kPrepTH + 2) * (kPrepTW + 2)];
     const size_t N = (size_t)W * (size_t)H;
-    prep_tile<kFast, kWide, false, kPrepThreads, kTileH>(
+    prep_tile<kFast, kWide, false, kPrepThreads, kPrepTH, kPrepTW>(
         depth + (size_t)f * N, recs + (size_t)(out0 + f) * P, W, H, P, K, F,
-        xyz ? xyz + (size_t)(out0 + f) * 3 * P : nullptr, tx * kTileW, ty * kTileH, sX, sY, sZ);
+        xyz ? xyz + (size_t)(out0 + f) * 3 * P : nullptr, tx * kPrepTW, ty * kPrepTH, sX, sY, sZ);
 }
 
 // ----------------------------------------------------------------- k_solve --
@@ -2728,7 +2738,7 @@ static int launch_prep(youth_icp_ctx* c, hipStream_t s, const int16_t* depth, in
         int rc = ensure_xyz(c);
         if (rc) return rc;
     }
-    const int tiles_x = (c->W + kTileW - 1) / kTileW, tiles_y = (c->H + kTileH - 1) / kTileH;
+    const int tiles_x = (c->W + kPrepTW - 1) / kPrepTW, tiles_y = (c->H + kPrepTH - 1) / kPrepTH;
     const long long rows = (long long)tiles_y * n_frames;
     const long long blocks = (long long)tiles_x * (c->prep_xcd_map == 2 ? (rows + 7) / 8 * 8 : rows);
     if (blocks > 0x7fffffffLL) return set_error(YOUTH_EINVAL, "launch_prep: %lld tiles", blocks);
