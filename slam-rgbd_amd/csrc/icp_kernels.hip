@@ -27,7 +27,6 @@
 // the IEEE path is compiled in.
 
 #include <hip/hip_runtime.h>
-#include <atomic>
 
 #include <stdarg.h>
 #include <stdint.h>
@@ -1856,72 +1855,6 @@ __device__ __forceinline__ int icp_claim(const IterState& is, int item, int tota
     return item;
 }
 
-// k_icp_coop's partials as data-tagged granules (MI355X_MICROARCH.md
-// "handoff-1to1": no drain, no counter): value v of row b is ONE 16-byte sc1
-// store {lo32, tag, hi32, tag} at piece b kPartStride + v, each 8-byte half
-// a {data, tag} granule.  A reader takes a piece once both halves carry this
-// iteration's tag (a torn or older piece fails the test and is re-read), so
-// the loads are the poll.  The sum is sum_pair_rows' tree value by value
-// (column j = rows j, j + 16, ... in batches of kBatch, then the 16 column
-// sums), so the totals are bit-identical to it.  Every spin is bounded
-// (kSpin polls, or *err set elsewhere): on timeout *stop is set.
-template <int kBatch, int kThreads>
-__device__ __forceinline__ double sum_pair_rows_tagged(__amdgpu_buffer_rsrc_t rpart, int nblk,
-                                                       double (*colsum)[kPartStride],
-                                                       unsigned tag, unsigned* err,
-                                                       unsigned spin_max, int* stop)
-{
-    for (int e = threadIdx.x; e < kSumCols * kPartStride; e += kThreads) {
-        const int j = e / kPartStride, v = e - j * kPartStride;
-        double sv = 0.0;
-        for (int bb = j; bb < nblk; bb += kBatch * kSumCols) {
-            u4v x[kBatch];
-#pragma unroll
-            for (int i = 0; i < kBatch; ++i) {
-                const int b = bb + i * kSumCols;
-                x[i] = b < nblk ? __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(
-                                                              rpart, (b * kPartStride + v) * 16, 0, 16))
-                                : u4v{0u, tag, 0u, tag};
-            }
-            unsigned spins = 0;
-            for (;;) {
-                bool bad = false;
-#pragma unroll
-                for (int i = 0; i < kBatch; ++i) bad |= (x[i].y != tag) | (x[i].w != tag);
-                if (!bad) break;
-                if (++spins > spin_max || ld_u32_sc1(err) != 0u) {
-                    __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    *stop = 1;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-                for (int i = 0; i < kBatch; ++i) {
-                    const int b = bb + i * kSumCols;
-                    if ((x[i].y != tag) | (x[i].w != tag))
-                        x[i] = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(
-                                                           rpart, (b * kPartStride + v) * 16, 0, 16));
-                }
-            }
-            double a[kBatch];
-#pragma unroll
-            for (int i = 0; i < kBatch; ++i) a[i] = __hiloint2double((int)x[i].z, (int)x[i].x);
-            sv += tree_sum<kBatch>(a);
-        }
-        colsum[j][v] = sv;
-    }
-    __syncthreads();
-    double tsum = 0.0;
-    const int t = threadIdx.x;
-    if (t < kNeq) {
-        double cc[kSumCols];
-#pragma unroll
-        for (int jj = 0; jj < kSumCols; ++jj) cc[jj] = colsum[jj][t];
-        tsum = tree_sum<kSumCols>(cc);
-    }
-    return tsum;
-}
-
 // Persistent ICP: ONE launch runs every iteration of every pair.  Work items
 // (k, p, c) = (iteration, pair, pixel chunk) are dequeued in that order from
 // one agent-scope counter; item (k, p, c) needs pair p's pose after k
@@ -2137,9 +2070,6 @@ struct CoopState {
     int chain;
     int tgt_slot[kCoopMaxChain], prep_slot[kCoopMaxChain];
     double* res_pair[kCoopMaxChain];
-    // partial tags: iteration k's rows carry tag0 + k + 1 (host: unique per
-    // launch across the process, never 0; the partials start zeroed)
-    unsigned tag0;
 };
 
 // Phase timestamps for tools/coopbench only (never in the product build):
@@ -2234,6 +2164,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
     const int p = blockIdx.x / G;
     const int c = blockIdx.x - p * G;
     const int N = W * H;
+    unsigned* cnt = cs.set + (size_t)p * kCoopShards * kCoopShardStride;
     unsigned* err = cs.set + kCoopErrWord;
     unsigned* prep_cnt = cs.set + kCoopPrepWords + (size_t)p * kCoopShardStride;
     // the prep counter this pair waits on: its own (prep_wait), or in a
@@ -2318,6 +2249,10 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
     const __amdgpu_buffer_rsrc_t rrec = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float4*>(recs + (size_t)tgt_frame * P), (short)0,
         (int)(P * sizeof(float4)), 0x00020000);
+    // shard s of this pair holds (k+1) x n_s after iteration k
+    const int my_shard = c & (kCoopShards - 1);
+    const unsigned n_s = lane < kCoopShards ? (unsigned)((G - lane + kCoopShards - 1) / kCoopShards)
+                                            : 0u;
     int32_t st_acc = 0;
     bool timeout = false;
     COOP_MARK(1, 15);  // source pixels staged
@@ -2379,36 +2314,55 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
             COOP_MARK(k, 11);
             if (!(lane & 1) && (lane >> 1) < kNeq) red[wave][lane >> 1] = tot;
         }
-        if (threadIdx.x == 0) sh_stop = 0;
         __syncthreads();
-        // rows of kPartStride 16-byte tagged pieces (sum_pair_rows_tagged)
-        double* part = partials + (size_t)(k & 1) * cs.n_pairs * G * kPartStride * 2 +
-                       (size_t)p * G * kPartStride * 2;
-        const __amdgpu_buffer_rsrc_t rpart = __builtin_amdgcn_make_buffer_rsrc(
-            part, (short)0, G * kPartStride * 16, 0x00020000);
-        const unsigned tag = cs.tag0 + (unsigned)k + 1u;
+        double* part = partials + (size_t)(k & 1) * cs.n_pairs * G * kPartStride +
+                       (size_t)p * G * kPartStride;
         COOP_MARK(k, 2);
-        if (wave == 0 && lane < kPartStride) {
-            // ---- publish this chunk's partial: one tagged sc1 piece per
-            // value, not drained (the readers' tag tests are the hand-off)
+        if (wave == 0) {
+            // ---- publish this chunk's partial (sc1, drained), then arrive
             double sum = 0.0;
-            if (lane < kNeq)
+            if (lane < kPartStride) {
+                if (lane < kNeq)
 #pragma unroll
-                for (int w = 0; w < kThreads / 64; ++w) sum += red[w][lane];
-            const u4v pc = {lo32(sum), tag, hi32(sum), tag};
-            __builtin_amdgcn_raw_buffer_store_b128(pc, rpart, (c * kPartStride + lane) * 16, 0, 16);
+                    for (int w = 0; w < kThreads / 64; ++w) sum += red[w][lane];
+                st_u64_sc1(part + (size_t)c * kPartStride + lane,
+                           (unsigned long long)__double_as_longlong(sum));
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0)
+                __hip_atomic_fetch_add(cnt + my_shard * kCoopShardStride, 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            COOP_MARK(k, 3);
+            // ---- wait for every workgroup of the pair: lanes 0..7 poll a shard each
+            const unsigned want = (unsigned)(k + 1) * n_s;
+            unsigned spins = 0;
+            int stop = 0;
+            for (;;) {
+                const unsigned have =
+                    lane < kCoopShards ? ld_u32_sc1(cnt + lane * kCoopShardStride) : 0u;
+                const bool done = __ballot(lane < kCoopShards && have < want) == 0ull;
+                if (done) break;
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > kCoopSpinMax || ld_u32_sc1(err) != 0u) {
+                    if (lane == 0)
+                        __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    stop = 1;
+                    break;
+                }
+            }
+            if (lane == 0) sh_stop = stop;
+            COOP_MARK(k, 4);
         }
-        COOP_MARK(k, 3);
-        COOP_MARK(k, 4);
+        __syncthreads();
         COOP_MARK(k, 5);
-        // ---- every workgroup sums the pair's partials in the same fixed
-        // order, each piece taken once it carries this iteration's tag
-        const double tsum =
-            sum_pair_rows_tagged<16, kThreads>(rpart, G, colsum, tag, err, kCoopSpinMax, &sh_stop);
         if (__builtin_amdgcn_readfirstlane(sh_stop)) {
             timeout = true;
             break;
         }
+        // ---- every workgroup sums the pair's partials in the same fixed order
+        const __amdgpu_buffer_rsrc_t rpart = __builtin_amdgcn_make_buffer_rsrc(
+            part, (short)0, G * kPartStride * (int)sizeof(double), 0x00020000);
+        const double tsum = sum_pair_rows<16>(rpart, G, colsum);
         COOP_MARK(k, 6);
         if (wave == 0) {
             if (lane < kNeq) sh_neq[lane] = tsum;
@@ -2633,8 +2587,6 @@ static int reduce_geometry(const youth_icp_ctx* c, int n_pairs, int* chunk_out)
     return nb;
 }
 
-// zeroed when allocated: k_icp_coop's tagged pieces start with tag 0, which
-// no launch uses (coop_tags)
 static int ensure_partials(youth_icp_ctx* c, size_t doubles)
 {
     if (doubles <= c->partials_cap) return YOUTH_OK;
@@ -2642,22 +2594,8 @@ static int ensure_partials(youth_icp_ctx* c, size_t doubles)
     c->d_partials = nullptr;
     c->partials_cap = 0;
     HIP_TRY(hipMalloc(&c->d_partials, doubles * sizeof(double)));
-    HIP_TRY(hipMemset(c->d_partials, 0, doubles * sizeof(double)));
     c->partials_cap = doubles;
     return YOUTH_OK;
-}
-
-// k_icp_coop's tag base for one launch of `iters` iterations: its rows carry
-// tag0 + 1 .. tag0 + iters.  One process-wide counter, so no two launches of
-// any contexts share a tag until it wraps (2^32 tags), and 0 is never used.
-static unsigned coop_tags(int iters)
-{
-    static std::atomic<unsigned> next{0u};
-    const unsigned n = (unsigned)iters + 1u;
-    for (;;) {
-        const unsigned t0 = next.fetch_add(n);
-        if (t0 + n > t0) return t0;  // no wrap inside [t0, t0 + n]: tags t0+1..t0+iters != 0
-    }
 }
 
 static int ensure_stats(youth_icp_ctx* c, int iters)
@@ -2967,7 +2905,7 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
                        const PrepJob* job)
 {
     const int iters = c->prm.iters;
-    int rc = ensure_partials(c, (size_t)2 * n_pairs * G * kPartStride * 2);
+    int rc = ensure_partials(c, (size_t)2 * n_pairs * G * kPartStride);
     if (rc) return rc;
     unsigned* set = c->d_coop + (size_t)c->coop_par * kCoopSetWords;
     unsigned* set_next = c->d_coop + (size_t)(c->coop_par ^ 1) * kCoopSetWords;
@@ -2990,7 +2928,6 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
                  n_pairs,  G,        npx,      job ? job->depth : nullptr,
                  job ? job->out0 : 0, job && job->wait ? 1 : 0, wide ? 1 : 0,
                  c->coop_res_host, tile_src ? 1 : 0};
-    cs.tag0 = coop_tags(iters);
     if (job && job->chain) {
         cs.chain = 1;
         for (int i = 0; i < kCoopMaxChain; ++i) {
@@ -3807,7 +3744,7 @@ static int reserve_for(youth_icp_ctx* c, int n_pairs)
     size_t need = (size_t)nb * n_pairs * kPartStride;
     int npx = 0, G = 0;
     if (coop_plan(c, n_pairs, &npx, &G))
-        need = std::max(need, (size_t)2 * n_pairs * G * kPartStride * 2);
+        need = std::max(need, (size_t)2 * n_pairs * G * kPartStride);
     int rc = ensure_partials(c, need);
     if (rc) return rc;
     return ensure_stats(c, c->prm.iters > 0 ? c->prm.iters : 1);

@@ -1,6 +1,7 @@
 // coopbench — where an iteration of k_icp_coop spends its time (one pair).
 //
-// Build: make -C tools coopbench      Run (GPU box): tools/coopbench [pairs] [px_per_lane]
+// Build: make -C tools coopbench
+// Run (GPU box): tools/coopbench [pairs] [px_per_lane (0: the plan's)] [W H iters]
 // Includes the production translation unit with YOUTH_COOP_PHASES, so thread
 // 0 of every workgroup stamps s_memrealtime (100 MHz) at 8 points of every
 // iteration: 0 start, 1 pixel loop done, 2 workgroup reduction done,
@@ -34,11 +35,13 @@ static double median(std::vector<double> v)
 int main(int argc, char** argv)
 {
     const int n = argc > 1 ? atoi(argv[1]) : 1;
-    if (argc > 2) setenv("YOUTH_ICP_COOP_PX", argv[2], 1);
+    if (argc > 2 && atoi(argv[2]) > 0) setenv("YOUTH_ICP_COOP_PX", argv[2], 1);
     setenv("YOUTH_ICP_COOP_MAX_PAIRS", "16", 1);
-    const int W = 640, H = 480, N = W * H;
+    const int W = argc > 4 ? atoi(argv[3]) : 640, H = argc > 4 ? atoi(argv[4]) : 480, N = W * H;
     youth_intrinsics K = youth_default_intrinsics(W, H);
     youth_icp_params prm = youth_default_params();
+    if (argc > 5) prm.iters = atoi(argv[5]);
+    if (prm.iters < 2 || prm.iters > 32) return 2;  // the phase buffer holds 32 iterations
     std::vector<int16_t> src((size_t)n * N), dst((size_t)n * N);
     std::vector<double> Tgt((size_t)n * 16);
     youth_synth_pairs(YOUTH_SYNTH_PAIR_SEED, 0, n, W, H, &K, YOUTH_SYNTH_NOISE | YOUTH_SYNTH_HOLES,
@@ -118,8 +121,8 @@ int main(int argc, char** argv)
     }
     const char* names[8] = {"pixel loop", "wg reduction", "publish+arrive", "poll (all arrived)",
                             "barrier", "sum partials", "solve+barrier", "loop back"};
-    printf("pairs %d  G %d  px/lane %d  (ns, medians over workgroups x iterations 1..%d x %d reps)\n",
-           n, G, npx, iters - 1, reps);
+    printf("%dx%d pairs %d  G %d  px/lane %d  (ns, medians over workgroups x iterations 1..%d x %d reps)\n",
+           W, H, n, G, npx, iters - 1, reps);
     double acc = 0;
     for (int s = 0; s < 8; ++s) {
         const double m = median(ph[s]);
