@@ -341,15 +341,14 @@ def roofline_icp(a, kt, n_pairs, W, H, concurrent=1):
     if traffic is not None:
         out["traffic_frac"] = traffic / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS
         out["traffic_over_algorithmic"] = traffic / alg
+    # what bounds k_icp, from same-box knockout timings: the
+    # share of the kernel's time each instruction group accounts for when it
+    # is removed.  The PMC issue account (below, "valu") is an upper estimate
+    # that exceeds 1 when the mixed stream overlaps better than the isolated
+    # forms, so it is reported, not used as the limiter.
+    out["limiter"] = "VALU issue + exposed memory latency (knockout shares)"
+    out["critical_path"] = KNOCKOUTS
     if tj and "valu_busy_frac" in tj:
-        # what bounds k_icp: VALU issue plus the memory latency
-        # each wave exposes.  valu_issue_frac is the issue ACCOUNT of the same
-        # PMC pass (instruction counts x isolated per-form costs): an upper
-        # estimate that exceeds 1 when the mixed stream overlaps better than
-        # the isolated forms; the knockouts measure what is on the critical path
-        out["limiter"] = "valu issue + exposed latency" if tj["valu_busy_frac"] > 0.8 else "hbm"
-        out["valu_issue_frac"] = tj["valu_busy_frac"]
-        out["critical_path"] = KNOCKOUTS
         out["valu"] = {k: tj[k] for k in ("valu_busy_frac", "valu_lane_ops_per_px_iteration",
                                           "valu_cycles_per_instruction", "effective_clock_ghz",
                                           "valu_busy_definition", "wave_state_frac",
