@@ -198,6 +198,65 @@ def test_assoc_extreme_poses(spec):
 
 
 @pytest.mark.parametrize("spec", SPECS)
+def test_projections_below_the_frame(spec):
+    """the survey arithmetic's projection has no explicit v' < H
+    test; a row past the frame is clamped to H and rejected because its
+    record index lands in the zeroed pad [N, P) or past the buffer.  Pinned
+    here against the oracle's explicit test: camera moves along +y and tilts
+    that push the lower rows of the scene to v' = H, H + 1, ... (counted
+    below with the survey formula in numpy float32): indices bit-exact, sums
+    within rel 1e-11, first-iteration match counts equal through k_icp_coop
+    and the persistent k_icp."""
+    oracle.set_spec(spec)
+    W, H = 640, 480
+    K = oracle.viewer_K(W, H)
+    src, dst, _ = youth_synth.pairs(78, 1)
+    X, Y, Z = oracle.backproject(src[0], K)
+    f32 = np.float32
+    Ts, at_H, below = [], 0, 0
+    for ty in np.linspace(0.002, 0.30, 12):
+        for tilt in (0.0, 2.0):
+            Tr = oracle.se3_exp(np.r_[np.deg2rad(tilt), 0.0, 0.0, 0.0, ty, 0.0])
+            T = Tr[:3].astype(np.float32)
+            qy = ((T[1, 0] * X + T[1, 1] * Y) + T[1, 2] * Z) + T[1, 3]
+            qz = ((T[2, 0] * X + T[2, 1] * Y) + T[2, 2] * Z) + T[2, 3]
+            with np.errstate(divide="ignore", invalid="ignore"):
+                fv = np.floor(((f32(K.fy) * qy) / qz + f32(K.cy)) + f32(0.5))
+            live = (Z > 0) & (qz > 0)
+            at_H += int((live & (fv == H)).sum())
+            below += int((live & (fv >= H)).sum())
+            Ts.append(Tr)
+    assert at_H > 100 and below > 10000, (at_H, below)
+    with youth_icp.IcpContext(W, H, 2, spec=spec) as ctx:
+        for draw, Tr in enumerate(Ts):
+            T32 = Tr[:3].astype(np.float32)
+            g_idx, g_neq = ctx.reduce(src[0], dst[0], T32)
+            assert np.array_equal(g_idx, oracle.associate(src[0], dst[0], T32, K)), draw
+            with oracle_like(ctx):
+                o_neq = oracle.reduce(src[0], dst[0], T32, K)
+            assert g_neq[28] == o_neq[28], draw
+            np.testing.assert_allclose(g_neq, o_neq, rtol=1e-11, atol=1e-9, err_msg=str(draw))
+    want = [int(oracle.align(src[0], dst[0], iters=1, T_init=T)[3][0, 0]) for T in Ts]
+    ds = torch.from_numpy(np.stack([src[0]] * 4)).cuda()
+    dd = torch.from_numpy(np.stack([dst[0]] * 4)).cuda()
+    torch.cuda.synchronize()
+    with youth_icp.IcpContext(W, H, 4, iters=1, spec=spec) as ctx:
+        for draw in range(0, len(Ts), 3):
+            ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), 1, T_init=Ts[draw][None])
+            assert int(ctx.get_stats(1, 1)[0][0, 0]) == want[draw], draw
+    os.environ["YOUTH_ICP_NO_COOP"] = "1"
+    try:
+        with youth_icp.IcpContext(W, H, 4, iters=1, spec=spec) as ctx:
+            for d0 in range(0, len(Ts), 4):
+                ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), 4,
+                                       T_init=np.stack(Ts[d0:d0 + 4]))
+                cnt, _ = ctx.get_stats(4, 1)
+                assert [int(v) for v in cnt[:, 0]] == want[d0:d0 + 4], d0
+    finally:
+        del os.environ["YOUTH_ICP_NO_COOP"]
+
+
+@pytest.mark.parametrize("spec", SPECS)
 @pytest.mark.parametrize("W,H,iters,n", [(640, 480, 10, 1), (640, 480, 10, 8),
                                          (640, 480, 10, 64), (1280, 960, 20, 1),
                                          (1280, 960, 20, 2)])
