@@ -877,6 +877,7 @@ def streamed_rate(a, frames, rel_batch, passes=5):
     v1, vp, vs = float(np.median(r_c)), float(np.median(r_py)), float(np.median(r_sync))
     vb = by_size[best_m]["value"]
     slam = slam_api_rate(a, frames, sync_by_m.get(youth_icp.TRACK_MAX_BATCH), passes=passes)
+    slam["c_producer"] = slam_rate_c(a, n, passes)
     return {"frames": n, "value": max(v1, vb), "unit": "frames/s", "slam_api": slam,
             "us_per_frame": 1e6 / max(v1, vb),
             "mode": f"micro-batches of {best_m} frames" if vb >= v1 else "one launch per frame",
@@ -970,6 +971,21 @@ def slam_api_rate(a, frames, rel_plan, passes=5):
     finally:
         youth_icp.stopSlamModule()
     return out
+
+
+def slam_rate_c(a, n, passes):
+    """The same backlogged / live processSlamFrame runs from a plain-C
+    producer thread (examples/slam_rate.c, its own process): the drop-in's
+    rate without Python in the producer."""
+    import subprocess
+    exe = os.path.join(ROOT, "slam-rgbd_amd", "slam_rate")
+    if not os.path.exists(exe):
+        return {"error": "slam_rate not built"}
+    r = subprocess.run([exe, str(n), str(passes), str(a.width), str(a.height)],
+                       capture_output=True, text=True, timeout=300)
+    if r.returncode != 0:
+        return {"error": f"rc {r.returncode}", "stderr_tail": r.stderr[-400:]}
+    return json.loads(r.stdout.strip().splitlines()[-1])
 
 
 def survey_noise_parity(a, ctx, main, n=16):

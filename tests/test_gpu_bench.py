@@ -96,6 +96,8 @@ def test_bench_single_gpu_contract():
     assert sa["value"] > 0 and sa["frames_recorded"] == sa["frames"] and sa["timestamps_in_order"]
     assert sa["world_pose_max_abs_diff_vs_track_frame_plan"] <= 1e-12
     assert sum(sa["batched_frames_per_pass"]) > 0
+    sc = sa["c_producer"]                         # the same from a plain-C producer
+    assert sc["value"] > 0 and sc["frames_recorded"] == sa["frames"] and sc["batched_frames"] > 0
     assert d["ranks"]["rccl_world_size"] == 1 and d["ranks"]["per_rank_ms"]["k_icp_ms"][0] > 0
 
 
