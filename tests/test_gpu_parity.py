@@ -20,10 +20,6 @@ from conftest import GOLDEN, lanes_of, oracle_like
 pytestmark = pytest.mark.gpu
 
 POSE_TOL = 1e-5
-# spec a9 lane32: the same pair aligned in launches that split its pixels into
-# lanes differently (other pairs per launch, other plans) differs by the fp32
-# rounding of the lane sums (observed <= 1.3e-6); one geometry is deterministic
-LANE32_GEOMETRY_TOL = 5e-6
 
 
 def _load(name):
@@ -173,24 +169,33 @@ def test_align_batch_640x480_matches_oracle():
         assert np.array_equal(assoc[p], oracle.associate(src[p], dst[p], Tg[p][:3]))
 
 
+def _per_chunk(src, dst, k, iters=10):
+    """The poses of the batch aligned as separate unpipelined calls of k pairs
+    (the last one ragged): the launch shapes a pipelined call of chunk k runs."""
+    out = []
+    for a in range(0, src.shape[0], k):
+        T, _ = youth_icp.align_batch(src[a:a + k], dst[a:a + k], iters=iters)
+        out.append(T)
+    return np.concatenate(out)
+
+
 @pytest.mark.parametrize("chunk", ["0", "8", "5"])
 def test_align_batch_pipelined_chunks(chunk, monkeypatch):
     """Host-buffer batch API with H2D of chunk k+1 overlapping the align of
     chunk k (YOUTH_ICP_BATCH_CHUNK; 21 pairs leaves a ragged last chunk):
-    poses within tolerance of the oracle and of the unpipelined call, and a
-    repeated call bit-identical.  (Spec a9's fp32 lane sums depend on how a
-    launch splits the pixels into lanes, which depends on the pairs per
-    launch: chunked and unchunked calls differ in the fp32 rounding of the
-    sums, LANE32_GEOMETRY_TOL; the exact reduction, in the fp64 order.)"""
+    bit-identical to the same chunks aligned by separate unpipelined calls
+    (spec a9's lane sums depend on the launch shape, i.e. on the pairs per
+    launch, so that is the reference with the same shapes), a repeat
+    bit-identical, and within 1e-5 of the oracle."""
     n = 21
     src, dst, _ = youth_synth.pairs(100, n, 160, 120)
     monkeypatch.setenv("YOUTH_ICP_BATCH_CHUNK", "0")
-    T_one, _ = youth_icp.align_batch(src, dst, iters=10)
+    T_ref = _per_chunk(src, dst, int(chunk) or n)
     monkeypatch.setenv("YOUTH_ICP_BATCH_CHUNK", chunk)
     T_chk, _ = youth_icp.align_batch(src, dst, iters=10)
     T_again, _ = youth_icp.align_batch(src, dst, iters=10)
     assert np.array_equal(T_chk, T_again)
-    assert float(np.abs(T_chk - T_one).max()) <= LANE32_GEOMETRY_TOL
+    assert np.array_equal(T_chk, T_ref)
     for p in (0, 7, 8, 20):
         T64, _, st, _ = oracle.align(src[p], dst[p], iters=10)
         assert _pose_err(T_chk[p], T64) <= POSE_TOL, p
@@ -199,16 +204,14 @@ def test_align_batch_pipelined_chunks(chunk, monkeypatch):
 def test_align_batch_default_chunks_ragged_tail(monkeypatch):
     """Default pipelining at 40 pairs: chunks of 16, 16 and 8 (persistent
     kernel, then a cooperative tail on the same context, workspace reserved
-    for both before the loop) equal the unpipelined call within the lane32
-    geometry tolerance (bit for bit with the exact reduction) and the oracle
-    within 1e-5."""
+    for both before the loop) equal those chunks aligned by separate
+    unpipelined calls bit for bit, and the oracle within 1e-5."""
     n = 40
     src, dst, _ = youth_synth.pairs(200, n)
     monkeypatch.delenv("YOUTH_ICP_BATCH_CHUNK", raising=False)
     T_chk, _ = youth_icp.align_batch(src, dst, iters=10)
     monkeypatch.setenv("YOUTH_ICP_BATCH_CHUNK", "0")
-    T_one, _ = youth_icp.align_batch(src, dst, iters=10)
-    assert float(np.abs(T_chk - T_one).max()) <= LANE32_GEOMETRY_TOL
+    assert np.array_equal(T_chk, _per_chunk(src, dst, 16))
     for p in (0, 15, 16, 32, 39):
         T64, _, st, _ = oracle.align(src[p], dst[p], iters=10)
         assert st == 0 and _pose_err(T_chk[p], T64) <= POSE_TOL, p
