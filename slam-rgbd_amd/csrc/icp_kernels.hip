@@ -195,12 +195,6 @@ constexpr int kSpecSurvey = YOUTH_SPEC_SURVEY;
 // The kernels' template parameter kSp is the VARIANT: bit 0 the arithmetic
 // (kSpecFma / kSpecSurvey), bit 1 (kRedLane32) the lane32 reduction.
 constexpr int kRedLane32 = 2;
-// k_icp's workgroups per CU (256 threads each) for the lane32 variants: its
-// fp32 accumulators need fewer VGPRs than the fp64 ones (108 vs 128 + spills)
-#ifndef YOUTH_ICP_LANE32_OCC
-#define YOUTH_ICP_LANE32_OCC 4
-#endif
-constexpr int kIcpLane32Occ = YOUTH_ICP_LANE32_OCC;
 constexpr int kVariants = 4;
 __host__ __device__ constexpr bool sp_survey(int v) { return (v & 1) == kSpecSurvey; }
 __host__ __device__ constexpr bool sp_lane32(int v) { return (v & kRedLane32) != 0; }
@@ -1331,78 +1325,6 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
     int v0 = i / W;
     int u0 = i - v0 * W;
     int cnt = 0;
-#if YOUTH_ICP_PIPE
-    // software-pipelined form (lane32, aligned, no association output): a
-    // step's four pixels in two halves of two, each half's matches and sums
-    // run while the next half's gathers are in flight (the same pixel state
-    // in registers as the plain loop: two halves instead of four pixels)
-    if constexpr (kAligned && !kAssoc && sp_lane32(kSp)) {
-        float facc[28];
-#pragma unroll
-        for (int q = 0; q < 28; ++q) facc[q] = 0.0f;
-        const __amdgpu_buffer_rsrc_t rdep = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<int16_t*>(sD), (short)0, W * H * (int)sizeof(int16_t), 0x00020000);
-        struct Half {
-            float qx[2], qy[2], qz[2], fu[2], fv[2];
-            LaneMask in[2];
-            f4v t[2];
-        };
-        // pixels h, h + 1 of the step at (uc0, vc0): projections, then gathers
-        auto project = [&](int d0, int d1, float uc, float vc, Half& o) {
-            const int dd[2] = {d0, d1};
-            int j[2];
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                float sx, sy, sz;
-                backproject_c<kFast>(dd[q], uc + (float)q, vc, K, F, sx, sy, sz);
-                xform_project<kSp>(T, sx, sy, sz, K, W, H, o.qx[q], o.qy[q], o.qz[q], o.fu[q],
-                                   o.fv[q], o.in[q], j[q]);
-            }
-#pragma unroll
-            for (int q = 0; q < 2; ++q)
-                o.t[q] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(
-                                                     rrec, (int)((unsigned)j[q] * 16u), 0, 0));
-        };
-        auto accumulate = [&](const Half& o) {
-#pragma unroll
-            for (int q = 0; q < 2; ++q)
-                cnt += __builtin_popcountll(match_accumulate<kSp, kFast, true>(
-                    o.qx[q], o.qy[q], o.qz[q], o.t[q], o.fu[q], o.fv[q], o.in[q], K, F, thr2,
-                    facc));
-        };
-        Half A, B;
-        bool pendB = false;
-        short4 d4 = i < end ? __builtin_bit_cast(
-                                  short4, __builtin_amdgcn_raw_buffer_load_b64(rdep, i * 2, 0, 0))
-                            : short4{};
-        for (; i < end; i += kRedStep) {
-            const float uc0 = (float)u0 - K.cx, vc0 = (float)v0 - K.cy;
-            const int d2 = d4.z, d3 = d4.w;
-            project(d4.x, d4.y, uc0, vc0, A);
-            // the next step's depth right behind A's gathers (0 past the frame),
-            // so the next step waits on it without waiting on B's gathers
-            d4 = __builtin_bit_cast(
-                short4, __builtin_amdgcn_raw_buffer_load_b64(rdep, (i + kRedStep) * 2, 0, 0));
-            asm volatile("" ::: "memory");
-            if (pendB) accumulate(B);
-            project(d2, d3, uc0 + 2.0f, vc0, B);
-            asm volatile("" ::: "memory");
-            accumulate(A);
-            pendB = true;
-            u0 += stepU;
-            v0 += stepV;
-            if (u0 >= W) {
-                u0 -= W;
-                ++v0;
-            }
-        }
-        if (pendB) accumulate(B);
-#pragma unroll
-        for (int q = 0; q < 28; ++q) acc[q] = (double)facc[q];
-        acc[28] += (threadIdx.x & 63) == 0 ? (double)cnt : 0.0;
-        return;
-    }
-#endif
     // lane32: this lane's fp32 sums over its whole share of the chunk,
     // converted to fp64 once at the end (acc enters zeroed)
     float facc[28];
@@ -1866,7 +1788,7 @@ __device__ __forceinline__ int icp_claim(const IterState& is, int item, int tota
 // (Dequeuing ahead from wave 1 so that waves 1-3 skip the second barrier
 // measured no faster: DESIGN.md §5.)
 template <int kSp, bool kFast, bool kAligned>
-__global__ __launch_bounds__(kRedThreads, sp_lane32(kSp) ? kIcpLane32Occ : 4) void k_icp(const int16_t* __restrict__ dsrc,
+__global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restrict__ dsrc,
                                                     const float4* __restrict__ recs, size_t P,
                                                     PairMap pm, int W, int H, Intr K, FastK F,
                                                     float thr2, double* __restrict__ partials,

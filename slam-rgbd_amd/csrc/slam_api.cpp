@@ -73,6 +73,8 @@ void buf_free(youth_frame_queue* q, youth_frame_queue::Item& it)
     it.cap = 0;
 }
 
+bool buf_alloc(youth_frame_queue* q, size_t n, bool want_pinned, youth_frame_queue::Item& it);
+
 // a buffer of >= n values: from the pool, else newly allocated (page-locked
 // while the queue's budget lasts)
 bool buf_get(youth_frame_queue* q, size_t n, youth_frame_queue::Item& it)
@@ -95,6 +97,24 @@ bool buf_get(youth_frame_queue* q, size_t n, youth_frame_queue::Item& it)
         if (want_pinned) q->pinned_bytes += n * sizeof(int16_t);
     }
     buf_free(q, old);  // too small for this frame size
+    return buf_alloc(q, n, want_pinned, it);
+}
+
+// a new buffer of n values (page-locked while the queue's budget lasts)
+bool buf_new(youth_frame_queue* q, size_t n, youth_frame_queue::Item& it)
+{
+    bool want_pinned = false;
+    {
+        std::lock_guard<std::mutex> lk(q->mu);
+        want_pinned = q->pinned && q->pinned_bytes + n * sizeof(int16_t) <= q->kPinnedBytes;
+        if (want_pinned) q->pinned_bytes += n * sizeof(int16_t);
+    }
+    return buf_alloc(q, n, want_pinned, it);
+}
+
+// the allocation behind buf_get / buf_new (want_pinned: budget already taken)
+bool buf_alloc(youth_frame_queue* q, size_t n, bool want_pinned, youth_frame_queue::Item& it)
+{
     it.buf = want_pinned ? youth_icp_host_alloc(n) : nullptr;
     it.pinned = it.buf != nullptr;
     if (want_pinned && !it.buf) {
@@ -132,6 +152,32 @@ int queue_take(youth_frame_queue* q, youth_frame_queue::Item& out)
     out = q->q.front();
     q->q.pop_front();
     return 1;
+}
+
+// Fill the pool with buffers of n values until it holds `count` of them
+// (page-locked while the budget lasts); smaller pooled buffers are freed.
+void queue_prefill(youth_frame_queue* q, size_t n, int count)
+{
+    std::vector<youth_frame_queue::Item> fresh, to_free;
+    {
+        std::lock_guard<std::mutex> lk(q->mu);
+        std::vector<youth_frame_queue::Item> keep;
+        for (auto& it : q->pool) (it.cap >= n ? keep : to_free).push_back(it);
+        q->pool.swap(keep);
+        count -= (int)q->pool.size();
+    }
+    free_all(q, to_free);
+    for (int i = 0; i < count; ++i) {
+        youth_frame_queue::Item it;
+        {
+            std::lock_guard<std::mutex> lk(q->mu);
+            if (q->pool.size() + fresh.size() >= q->kPoolMax) break;
+        }
+        if (!buf_new(q, n, it)) break;
+        fresh.push_back(it);
+    }
+    std::lock_guard<std::mutex> lk(q->mu);
+    for (auto& it : fresh) q->pool.push_back(it);
 }
 
 void queue_release(youth_frame_queue* q, youth_frame_queue::Item& it)
@@ -292,6 +338,11 @@ youth_frame_queue* g_queue = nullptr;
 std::mutex g_state_mu;  // run/stop hand-off for algorithmModule
 std::condition_variable g_state_cv;
 
+// processSlamFrame wakes the idle worker (no polling interval between a
+// camera frame's arrival and its upload)
+std::mutex g_wake_mu;
+std::condition_variable g_wake_cv;
+
 // configuration from initSlamModule
 youth_intrinsics g_cfg_K;
 int g_cfg_W = 0, g_cfg_H = 0;
@@ -401,7 +452,15 @@ void worker_main(int device)
                 continue;
             }
             g_busy.store(false);
-            std::this_thread::sleep_for(std::chrono::milliseconds(1));
+            {
+                // the predicate re-checks the queue under g_wake_mu, which
+                // processSlamFrame takes before notifying: no lost wake-up
+                // (system_clock: pthread_cond_timedwait, which ThreadSanitizer
+                // intercepts; a steady_clock wait_for is pthread_cond_clockwait)
+                std::unique_lock<std::mutex> lk(g_wake_mu);
+                g_wake_cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(20),
+                                     [] { return !g_process.load() || youth_queue_size(g_queue) > 0; });
+            }
             continue;
         }
         const int w = items[0].w, h = items[0].h;
@@ -425,6 +484,9 @@ void worker_main(int device)
                 continue;
             }
             if (batch > 1) youth_icp_track_set_batch(ctx, batch);
+            // page-locked buffers for this size up front: a backlog keeps
+            // about queue (11) + in flight (2 batch) + one batch of frames
+            queue_prefill(g_queue, (size_t)w * h, 11 + 3 * batch);
         }
         const size_t N = (size_t)w * h;
         // the micro-batch: frames of this size already waiting, up to `batch`
@@ -624,6 +686,10 @@ int processSlamFrame(const int16_t* depth_data, const uint8_t* color_data, int w
         return 0;
     }
     const int rc = youth_queue_push(g_queue, depth_data, width, height, timestamp);
+    if (rc >= 0) {
+        std::lock_guard<std::mutex> lk(g_wake_mu);
+        g_wake_cv.notify_one();
+    }
     if (rc < 0) {
         fprintf(stderr, "youth_icp: processSlamFrame: enqueue failed (%d)\n", rc);
         return 0;
