@@ -55,20 +55,23 @@ namespace {
 // clamped fetch or a float4 load past N reads an invalid point (z = 0).
 // Sources are read straight from the caller's int16 depth.
 constexpr int kTileW = 64;
-// k_prep tiles 64 x 48 by 512-thread workgroups: four per CU fill all 32
-// wave slots (LDS 39.6 KB each) with 4 % halo rows.  Per 512 frames: 64 x 24
-// by 256 threads (seven per CU, LDS-limited) 617 us, 64 x 40 / 512 603 us,
-// 64 x 48 / 512 593 us, 64 x 80 and 64 x 96 by 1024 threads 625-643 us
-// (profiles/r02/ab_s44.txt, ab_s45.txt); fewer workgroups per CU cost more
-// (ab_s43.txt: 7 -> 6 per CU +8 %)
+// k_prep tiles 128 x 24 by 512-thread workgroups: four per CU fill all 32
+// wave slots (LDS 40.6 KB each).  A 128-px row touches 2 lines of its own
+// and 2 of its neighbours' where a 64-px row touched 1 + 2, so the depth
+// over-fetch drops from 2.8x to 1.9x: k_prep's PMC traffic 1.21 -> 1.105x of
+// its 18 B/px, and 586 -> 582 us per 512 frames (profiles/r04/ab_r4c.txt,
+// prep128x24_pmc.txt).  Also measured: 128 x 16 650 us (1.11x), 256 x 12
+// 747 us (1.07x; three per CU, LDS-limited); earlier 64 x 48 593 us, 64 x 24 by
+// 256 threads 617 us, 64 x 80 / 1024 625 us (profiles/r02/ab_s44.txt,
+// ab_s45.txt); fewer workgroups per CU cost more (ab_s43.txt: 7 -> 6 per CU +8 %)
 constexpr int kPrepThreads = 512;
-// k_prep's own tile (A/B knobs; k_icp_coop's fused prep keeps kTileW-wide
-// tiles, whose shape its lane partition and prep counters assume)
+// k_prep's own tile (k_icp_coop's fused prep keeps kTileW-wide tiles, whose
+// shape its lane partition and prep counters assume); -D knobs for A/B
 #ifndef YOUTH_PREP_TW
-#define YOUTH_PREP_TW 64
+#define YOUTH_PREP_TW 128
 #endif
 #ifndef YOUTH_PREP_TH
-#define YOUTH_PREP_TH 48
+#define YOUTH_PREP_TH 24
 #endif
 constexpr int kPrepTW = YOUTH_PREP_TW;
 constexpr int kPrepTH = YOUTH_PREP_TH;
