@@ -29,30 +29,47 @@ int main(int argc, char** argv)
     unsigned* d_dbg;
     (void)hipMalloc(&d_s, N * 2);
     (void)hipMalloc(&d_d, N * 2);
-    (void)hipMalloc(&d_dbg, (16 + 512 * 16) * 4);
+    const size_t dbg_words = 64 + 256 * 64;
+    (void)hipMalloc(&d_dbg, dbg_words * 4);
     (void)hipMemcpy(d_s, src.data(), N * 2, hipMemcpyHostToDevice);
     (void)hipMemcpy(d_d, dst.data(), N * 2, hipMemcpyHostToDevice);
     (void)hipMemcpyToSymbol(HIP_SYMBOL(tag_dbg), &d_dbg, sizeof(d_dbg));
+    printf("poll loads: aux %d\n", POLL_AUX);
     for (int r = 0; r < reps; ++r) {
-        (void)hipMemset(d_dbg, 0, (16 + 512 * 16) * 4);
+        (void)hipMemset(d_dbg, 0, dbg_words * 4);
         const int rc = youth_icp_align_pairs_device(c, d_s, d_d, 1, nullptr, nullptr, nullptr);
         (void)hipDeviceSynchronize();
         double T64[16];
         float T32[12];
         int32_t st = -1;
         youth_icp_get_poses(c, 1, T64, T32, &st);
-        std::vector<unsigned> h(16 + 512 * 16);
+        std::vector<unsigned> h(dbg_words);
         (void)hipMemcpy(h.data(), d_dbg, h.size() * 4, hipMemcpyDeviceToHost);
         const int G = c->last_coop_G;
-        printf("rep %d: rc %d status %d  G %d px %d  timeout records %u  tag0 base unknown\n", r, rc,
-               st, G, c->last_coop_px, h[0]);
-        for (unsigned s = 0; s < std::min(h[0], 12u); ++s) {
-            const unsigned* q = &h[16 + s * 16];
-            printf("  wg %4u thr %3u bb %3u v %2u tag %u spins %u | row %3u of %u read {x %08x tag %u z %08x tag %u}"
-                   "  re-read sc0sc1 {tag %u tag %u x %08x} %s\n",
-                   q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[11], q[7], q[8], q[9], q[10], q[12], q[13],
-                   q[14], q[15] == 0xabcd1234u ? "" : "(bad record)");
+        printf("rep %d: rc %d status %d  G %d px %d  timeout records %u\n", r, rc, st, G,
+               c->last_coop_px, h[0]);
+        unsigned waves[64] = {};
+        int nw = 0;
+        for (unsigned s2 = 0; s2 < std::min(h[0], 256u); ++s2) {
+            const unsigned* q = &h[64 + s2 * 64];
+            const unsigned wv = q[0] * 8 + q[1] / 64;
+            bool seen = false;
+            for (int k = 0; k < nw; ++k) seen |= waves[k] == wv;
+            if (!seen && nw < 64) waves[nw++] = wv;
+            if (s2 < 6 || !seen) {
+                printf("  wg %4u thr %3u bb %3u v %2u tag %u spins %u badmask %04x\n    poll saw:", q[0],
+                       q[1], q[2], q[3], q[4], q[5], q[6]);
+                for (int i = 0; i < 16; ++i) printf(" %u", q[8 + i]);
+                printf("\n    sys now: ");
+                for (int i = 0; i < 16; ++i) printf(" %u", q[24 + i]);
+                printf("\n    poll now:");
+                for (int i = 0; i < 16; ++i) printf(" %u", q[40 + i]);
+                printf("%s\n", q[63] == 0xabcd1234u ? "" : " (bad record)");
+            }
         }
+        printf("  waves with timeouts: %d:", nw);
+        for (int k = 0; k < nw; ++k) printf(" wg%u.w%u", waves[k] / 8, waves[k] % 8);
+        printf("\n");
         // the rows as they sit in memory now (both parity buffers)
         const size_t words = (size_t)2 * G * kPartStride * 4;
         std::vector<unsigned> part(words);
