@@ -295,12 +295,17 @@ def load_pmc(a, W, H):
     return tj, os.path.relpath(a.traffic_json, ROOT)
 
 
-# Same-box knockout timings of k_icp (profiles/r03/ab_knockout.txt): the share
-# of the kernel's time each instruction group accounts for when it is removed
-# (timing-only builds), next to the share the issue account prices it at.
+# Same-box knockout timings of k_icp: the share of the kernel's time each
+# instruction group accounts for when it is removed (timing-only builds, wrong
+# sums).  The default lane32 reduction's update (28 fp32 FMAs per pixel) is
+# 2.2-2.8 % of k_icp (profiles/r04/ab_r4a.txt: 4724 -> 4622 us, 4699 -> 4569
+# us); the exact form's fp64 update was 16 % (profiles/r03/ab_knockout.txt),
+# next to the 32 % the issue account priced it at.
 KNOCKOUTS = {
-    "source": "profiles/r03/ab_knockout.txt",
-    "fp64_update": {"measured_time_share": 0.16, "issue_account_share": 0.32},
+    "source": "profiles/r04/ab_r4a.txt (lane32), profiles/r03/ab_knockout.txt (exact)",
+    "lane32_fp32_update": {"measured_time_share": 0.025, "reduction": "lane32 (default)"},
+    "exact_fp64_update": {"measured_time_share": 0.16, "issue_account_share": 0.32,
+                          "reduction": "exact (opt-in)"},
     "target_int_to_float": {"measured_time_share": 0.005, "issue_account_share": 0.033},
 }
 

@@ -34,6 +34,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -4107,6 +4108,27 @@ void youth_icp_host_free(int16_t* p)
     if (p) (void)hipHostFree(p);
 }
 
+// A collect waits for its frame by polling the event for up to 2 ms before
+// the runtime's blocking wait: a sleeping wait's wake-up cost a backlogged
+// SLAM worker up to ~0.6 ms per micro-batch (profiles/r04/slamtrace_r4k.txt).
+// YOUTH_ICP_TRACK_WAIT=sync keeps the blocking wait only (A/B).
+static hipError_t track_wait(hipEvent_t ev)
+{
+    static const bool poll = [] {
+        const char* e = getenv("YOUTH_ICP_TRACK_WAIT");
+        return !(e && strcmp(e, "sync") == 0);
+    }();
+    if (poll) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            const hipError_t r = hipEventQuery(ev);
+            if (r != hipErrorNotReady) return r;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+        }
+    }
+    return hipEventSynchronize(ev);
+}
+
 int youth_icp_track_collect(youth_icp_ctx* c, double* T_rel, int* has_ref)
 {
     if (!c || !T_rel) return set_error(YOUTH_EINVAL, "track_collect: bad arguments");
@@ -4116,7 +4138,7 @@ int youth_icp_track_collect(youth_icp_ctx* c, double* T_rel, int* has_ref)
     auto& q = c->trk[c->trk_head];
     c->trk_head = (c->trk_head + 1) % c->trk_cap;
     --c->trk_n;
-    HIP_TRY(hipEventSynchronize(q.ev));
+    HIP_TRY(track_wait(q.ev));
     if (has_ref) *has_ref = q.has_ref;
     if (!q.has_ref) {
         for (int i = 0; i < 16; ++i) T_rel[i] = (i % 5) == 0 ? 1.0 : 0.0;

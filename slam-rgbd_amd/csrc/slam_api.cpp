@@ -51,6 +51,10 @@ struct youth_frame_queue {
     static constexpr size_t kPoolMax = 48;  // free buffers kept
     std::mutex mu;
     std::deque<Item> q;
+    // q.size(), stored under mu after every change: youth_queue_size reads
+    // it without the lock, so a producer polling the depth (the reference's
+    // logger waits on it) never contends with the worker's takes
+    std::atomic<int> depth{0};
     std::vector<Item> pool;
     int high = 10, low = 5;
     bool pinned = false;      // allocate page-locked buffers (SLAM module queue)
@@ -151,6 +155,7 @@ int queue_take(youth_frame_queue* q, youth_frame_queue::Item& out)
     if (q->q.empty()) return 0;
     out = q->q.front();
     q->q.pop_front();
+    q->depth.store((int)q->q.size(), std::memory_order_release);
     return 1;
 }
 
@@ -240,6 +245,7 @@ int youth_queue_push(youth_frame_queue* q, const int16_t* depth, int width, int 
                 ++dropped;
             }
         }
+        q->depth.store((int)q->q.size(), std::memory_order_release);
     }
     free_all(q, to_free);
     return dropped;
@@ -257,6 +263,7 @@ int youth_queue_pop(youth_frame_queue* q, int16_t* depth_out, size_t cap, int* w
         if ((size_t)f.w * (size_t)f.h > cap || !depth_out) return YOUTH_EINVAL;
         it = f;
         q->q.pop_front();
+        q->depth.store((int)q->q.size(), std::memory_order_release);
     }
     memcpy(depth_out, it.buf, (size_t)it.w * it.h * sizeof(int16_t));
     if (width) *width = it.w;
@@ -269,8 +276,7 @@ int youth_queue_pop(youth_frame_queue* q, int16_t* depth_out, size_t cap, int* w
 int youth_queue_size(youth_frame_queue* q)
 {
     if (!q) return 0;
-    std::lock_guard<std::mutex> lk(q->mu);
-    return (int)q->q.size();
+    return q->depth.load(std::memory_order_acquire);
 }
 
 void youth_queue_clear(youth_frame_queue* q)
@@ -281,6 +287,7 @@ void youth_queue_clear(youth_frame_queue* q)
         std::lock_guard<std::mutex> lk(q->mu);
         for (auto& it : q->q) pool_put_locked(q, it, to_free);
         q->q.clear();
+        q->depth.store(0, std::memory_order_release);
     }
     free_all(q, to_free);
 }
@@ -350,6 +357,10 @@ bool g_cfg_has_yaml = false;
 
 // tracker state (worker thread owns ctx; trajectory guarded by g_slam_mu)
 std::vector<PoseRec> g_traj;
+// g_traj.size(), stored under g_slam_mu after every change: a host polling
+// for its pose (youth_slam_trajectory_length) does not take the lock the
+// worker records every pose under
+std::atomic<int> g_traj_len{0};
 int g_last_points = 0;
 
 void mat_mul4(const double* A, const double* B, double* C)
@@ -399,14 +410,17 @@ void worker_main(int device)
     struct Pending {
         uint32_t ts;
         int npts;   // valid pixels (counted for the last frame of a submission, else -1)
+        bool last;  // the last frame of its submission
         Item item;  // its buffer, in use by the H2D until the frame is collected
     };
     std::deque<Pending> pend;  // submitted, not yet collected (oldest first)
+    int subs = 0;              // submissions in pend
     // collect the oldest submitted frame; record its pose unless a reset
     // arrived since it was submitted; its buffer goes back to the pool
     auto finish_one = [&](bool record) {
         Pending pr0 = pend.front();
         pend.pop_front();
+        subs -= pr0.last;
         double T_rel[16];
         int has_ref = 0;
         const int st = youth_icp_track_collect(ctx, T_rel, &has_ref);
@@ -426,6 +440,7 @@ void worker_main(int device)
             double I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
             memcpy(T_w_ref, I, sizeof(I));
             g_traj.clear();
+            g_traj_len.store(0, std::memory_order_release);
         } else {
             // P_ref = T_rel P_new  =>  T_w_new = T_w_ref * T_rel
             mat_mul4(T_w_ref, T_rel, T_w_ref);
@@ -434,6 +449,7 @@ void worker_main(int device)
         pr.ts = pr0.ts;
         memcpy(pr.T, T_w_ref, sizeof(pr.T));
         g_traj.push_back(pr);
+        g_traj_len.store((int)g_traj.size(), std::memory_order_release);
         if (pr0.npts >= 0) g_last_points = pr0.npts;
     };
     while (g_process.load()) {
@@ -489,6 +505,16 @@ void worker_main(int device)
             queue_prefill(g_queue, (size_t)w * h, 11 + 3 * batch);
         }
         const size_t N = (size_t)w * h;
+        // two submissions in flight: with two queued, finish the oldest
+        // before gathering the batch (the queue fills meanwhile, so a backlog
+        // goes out in full micro-batches rather than as many small launches
+        // each costing a full one)
+        if (subs >= 2)
+            while (!pend.empty()) {
+                const bool last = pend.front().last;
+                finish_one(true);
+                if (last) break;
+            }
         // the micro-batch: frames of this size already waiting, up to `batch`
         // in all (one of another size, or taken after a reset, is held for
         // the next round)
@@ -503,7 +529,7 @@ void worker_main(int device)
                 held = true;
             }
         }
-        // two submissions in flight: frames, or micro-batches
+        // the tracker holds 2 batch frames in flight
         while (!pend.empty() && (int)pend.size() + m > 2 * batch) finish_one(true);
         const long long chained0 = youth_icp_track_chained_frames(ctx);
         bool pinned = true;
@@ -532,10 +558,11 @@ void worker_main(int device)
         if (rc < 0) fprintf(stderr, "youth_icp: tracking failed: %s\n", youth_icp_last_error());
         for (int i = 0; i < m; ++i) {
             if (i < sent)
-                pend.push_back(Pending{items[i].ts, i == m - 1 ? npts : -1, items[i]});
+                pend.push_back(Pending{items[i].ts, i == m - 1 ? npts : -1, i == sent - 1, items[i]});
             else
                 queue_release(g_queue, items[i]);
         }
+        subs += sent > 0;
         if (batch == 1 && pend.size() == 2) finish_one(true);
     }
     while (ctx && !pend.empty()) finish_one(true);
@@ -641,6 +668,7 @@ void initSlamModule(const char* config_file, const char* vocabulary_file)
     }
     youth_queue_clear(g_queue);
     g_traj.clear();
+    g_traj_len.store(0, std::memory_order_release);
     g_last_points = 0;
     g_process.store(true);
     g_batched.store(0);
@@ -740,16 +768,13 @@ void resetSlam(void)
         std::lock_guard<std::mutex> lk(g_slam_mu);
         g_reset.store(true);
         g_traj.clear();
+        g_traj_len.store(0, std::memory_order_release);
         g_last_points = 0;
     }
     fprintf(stderr, "youth_icp: SLAM system reset\n");
 }
 
-int youth_slam_trajectory_length(void)
-{
-    std::lock_guard<std::mutex> lk(g_slam_mu);
-    return (int)g_traj.size();
-}
+int youth_slam_trajectory_length(void) { return g_traj_len.load(std::memory_order_acquire); }
 
 int youth_slam_get_trajectory(int n, uint32_t* timestamps, double* T_wc)
 {

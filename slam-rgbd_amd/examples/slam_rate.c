@@ -13,6 +13,8 @@
  *               latency).
  *
  * Prints one JSON object: frames/s per pass (backlogged), the median, the
+ * producer's mean time inside processSlamFrame per pass (the frame copy), each
+ * pass's CLOCK_MONOTONIC window, the
  * live latency median / p90 in microseconds, frames aligned in chained
  * launches, and a checksum of the last pass's world poses.
  *
@@ -62,21 +64,27 @@ int main(int argc, char** argv)
     /* warm: the worker's context, its plan and the page-locked queue pool */
     for (int k = 0; k < n && k < 24; ++k) processSlamFrame(frames + (size_t)k * N, NULL, W, H, k);
     youth_slam_wait_idle(20000);
-    double rate[64];
+    double rate[64], push_us[64], win[64][2];
     long long batched = 0;
     for (int p = 0; p < passes; ++p) {
         resetSlam();
         youth_slam_wait_idle(20000);
         const long long b0 = youth_slam_batched_frames();
         const double t0 = now_s();
+        double in_push = 0.0;
         for (int k = 0; k < n; ++k) {
             while (youth_slam_queue_size() >= 10) {
             }
+            const double tp = now_s();
             if (processSlamFrame(frames + (size_t)k * N, NULL, W, H, (uint32_t)k) != 1) return 5;
+            in_push += now_s() - tp;
         }
         while (youth_slam_trajectory_length() < n) {
         }
-        rate[p] = n / (now_s() - t0);
+        win[p][0] = t0;
+        win[p][1] = now_s();
+        rate[p] = n / (win[p][1] - t0);
+        push_us[p] = in_push * 1e6 / n;
         batched += youth_slam_batched_frames() - b0;
     }
     const int got = youth_slam_get_trajectory(n, NULL, T);
@@ -101,6 +109,10 @@ int main(int argc, char** argv)
            "\"pass_values\": [",
            n, W, H, sorted[passes / 2]);
     for (int p = 0; p < passes; ++p) printf("%s%.1f", p ? ", " : "", rate[p]);
+    printf("], \"push_us_per_frame\": [");
+    for (int p = 0; p < passes; ++p) printf("%s%.1f", p ? ", " : "", push_us[p]);
+    printf("], \"pass_windows_s\": [");
+    for (int p = 0; p < passes; ++p) printf("%s[%.6f, %.6f]", p ? ", " : "", win[p][0], win[p][1]);
     printf("], \"batched_frames\": %lld, \"frames_recorded\": %d, \"pose_checksum\": %.17g, "
            "\"live_latency_us_median\": %.1f, \"live_latency_us_p90\": %.1f, "
            "\"producer\": \"one C thread, processSlamFrame\"}\n",
