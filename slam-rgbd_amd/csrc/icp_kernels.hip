@@ -535,29 +535,83 @@ __device__ __forceinline__ void prep_tile(const int16_t* __restrict__ dep, float
     const int tx = threadIdx.x % kTW;
     const int ty = threadIdx.x / kTW;
     if (kWide) {
-        // W % 4 == 0 (and an 8-byte-aligned frame): columns [x0-4, x0+68) as
-        // 18 aligned 8-byte words per halo row; each word's 4 pixels are all
-        // inside or all outside the image, so no lane straddles an edge.
-        constexpr int kWords = (kTW + 8) / 4;  // 18 at 64
-        for (int e = threadIdx.x; e < kLH * kWords; e += kThreads) {
+        // W % 4 == 0 (and an 8-byte-aligned frame): the tile's own columns
+        // [x0, x0 + kTW) as kTW / 4 aligned 8-byte words per halo row (each
+        // word's 4 pixels all inside or all outside the image, so no lane
+        // straddles an edge and every pixel of a word is stored), then the two
+        // edge columns x0 - 1 and x0 + kTW one pixel per lane.  An outside
+        // pixel back-projects d = 0 at its own (u, v), as before.
+        // Words load through a buffer descriptor over the frame: a row
+        // outside the image or a word past the right edge takes offset -1,
+        // which the descriptor's range check returns as 0 (no branch, no
+        // 64-bit address arithmetic).  The edge pixels are loaded first, so
+        // their latency overlaps the words' instead of adding a round trip
+        // before the barrier.
+        static_assert(2 * kLH <= kThreads, "one edge pixel per thread");
+        const bool edge = threadIdx.x < 2 * kLH;
+        const int ely = threadIdx.x >> 1, eright = threadIdx.x & 1;
+        const int egy = y0 - 1 + ely, egx = eright ? x0 + kTW : x0 - 1;
+        const __amdgpu_buffer_rsrc_t rdep = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<int16_t*>(dep), (short)0, W * H * (int)sizeof(int16_t), 0x00020000);
+        const bool ein = edge & ((unsigned)egy < (unsigned)H) & ((unsigned)egx < (unsigned)W);
+        unsigned short dedge =
+            __builtin_amdgcn_raw_buffer_load_b16(rdep, ein ? (egy * W + egx) * 2 : -1, 0, 0);
+        // every word of the thread is requested before the first is used
+        // (kIt loads in flight: 2 at 128 x 24 by 512 threads)
+        constexpr int kWords = kTW / 4;  // 32 at 128: a shift, not a divide
+        constexpr int kIt = (kLH * kWords + kThreads - 1) / kThreads;
+        short4 wd[kIt];
+#pragma unroll
+        for (int it = 0; it < kIt; ++it) {
+            const int e = threadIdx.x + it * kThreads;
+            const int ly = e / kWords;
+            const int gy = y0 - 1 + ly;
+            const int c = x0 + 4 * (e - ly * kWords);
+            const bool inside = (e < kLH * kWords) & ((unsigned)gy < (unsigned)H) & (c < W);
+            wd[it] = __builtin_bit_cast(
+                short4, __builtin_amdgcn_raw_buffer_load_b64(rdep, inside ? (gy * W + c) * 2 : -1, 0, 0));
+        }
+        // the loads above stay where they are: each result passes through an
+        // empty asm here (the frame pointer is __restrict__, so a memory
+        // clobber would not pin them), one wait for all of them
+#pragma unroll
+        for (int it = 0; it < kIt; ++it) {
+            unsigned long long v = __builtin_bit_cast(unsigned long long, wd[it]);
+            asm volatile("" : "+v"(v));
+            wd[it] = __builtin_bit_cast(short4, v);
+        }
+        {
+            unsigned v = dedge;
+            asm volatile("" : "+v"(v));
+            dedge = (unsigned short)v;
+        }
+#pragma unroll
+        for (int it = 0; it < kIt; ++it) {
+            const int e = threadIdx.x + it * kThreads;
+            if (e >= kLH * kWords) break;
             const int ly = e / kWords;
             const int m = e - ly * kWords;
             const int gy = y0 - 1 + ly;
-            const int c = x0 - 4 + 4 * m;
-            short4 d4 = make_short4(0, 0, 0, 0);
-            if (gy >= 0 && gy < H && c >= 0 && c < W)
-                d4 = *reinterpret_cast<const short4*>(dep + (size_t)gy * W + c);
+            const int c = x0 + 4 * m;
+            const short4 d4 = wd[it];
             const int dv[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const int lx = 4 * m - 3 + q;  // LDS column of pixel c + q
-                if (lx < 0 || lx >= kLW) continue;
+                const int lx = 4 * m + 1 + q;  // LDS column of pixel c + q
                 float x, y, z;
                 backproject<kFast>(dv[q], c + q, gy, K, F, x, y, z);
                 sX[ly * kLW + lx] = x;
                 sY[ly * kLW + lx] = y;
                 sZ[ly * kLW + lx] = z;
             }
+        }
+        if (edge) {
+            float x, y, z;
+            backproject<kFast>((int)(short)dedge, egx, egy, K, F, x, y, z);
+            const int lx = eright ? kLW - 1 : 0;
+            sX[ely * kLW + lx] = x;
+            sY[ely * kLW + lx] = y;
+            sZ[ely * kLW + lx] = z;
         }
     } else {
         for (int e = threadIdx.x; e < kLH * kLW; e += kThreads) {
@@ -642,10 +696,13 @@ __device__ __forceinline__ void prep_tile(const int16_t* __restrict__ dep, float
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, rec), rrec,
                                                    (int)(i * sizeof(float4)), 0, 16);
         } else {
-            // non-temporal: k_prep's 16 B/px stream of records is read back
-            // by k_icp only after the whole batch is written (610 vs 626 us
-            // per 512 frames, profiles/r02/ab_s30.txt, ab_s31.txt)
-            __builtin_nontemporal_store(__builtin_bit_cast(u4v, rec), reinterpret_cast<u4v*>(R) + i);
+            // non-temporal (aux 2: nt): k_prep's 16 B/px stream of records is
+            // read back by k_icp only after the whole batch is written (610 vs
+            // 626 us per 512 frames, profiles/r02/ab_s30.txt, ab_s31.txt);
+            // through the frame's buffer descriptor: a 32-bit byte offset
+            // instead of 64-bit address arithmetic per record
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, rec), rrec,
+                                                   (int)(i * sizeof(float4)), 0, 2);
         }
     }
 }
