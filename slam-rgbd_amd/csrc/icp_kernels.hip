@@ -1407,7 +1407,8 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
         LaneMask in[4];
         int j[4];
         // a lane's four pixels share one row when kAligned: centred
-        // coordinates by exact additions (uc0 + q == (float)(u0 + q) - cx)
+        // coordinates by exact additions (uc0 + q == (float)(u0 + q) - cx,
+        // which the host checked for these intrinsics: centred_exact)
         const float uc0 = (float)u0 - K.cx, vc0 = (float)v0 - K.cy;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -2444,6 +2445,7 @@ struct youth_icp_ctx {
     Intr K{};
     FastK F{};
     bool fast = false;  // verified 2-op back-projection division
+    bool centred_exact = true;  // aligned loop's centred columns exact (centred_exact)
     int spec = kSpecSurvey;  // spec a7/a8 arithmetic (youth_icp_set_spec, YOUTH_ICP_SPEC)
     youth_icp_params prm{};
     hipStream_t stream = nullptr;
@@ -2722,7 +2724,8 @@ static int launch_reduce(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, P
         if (rc) return rc;
     }
     const float thr2 = c->prm.dist_thresh * c->prm.dist_thresh;
-    const bool aligned = (reinterpret_cast<uintptr_t>(dsrc) % 8 == 0) && (c->W % 4 == 0);
+    const bool aligned = (reinterpret_cast<uintptr_t>(dsrc) % 8 == 0) && (c->W % 4 == 0) &&
+                           c->centred_exact;
     dim3 grid(nb, n_pairs);
     EventPair ep{};
     rc = ev_begin(c, s, &ep, 0);
@@ -3039,7 +3042,8 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
         const int nb = reduce_geometry(c, n_pairs, &chunk);
         rc = ensure_partials(c, (size_t)nb * n_pairs * kPartStride);
         if (rc) return rc;
-        const bool aligned = (reinterpret_cast<uintptr_t>(dsrc) % 8 == 0) && (c->W % 4 == 0);
+        const bool aligned = (reinterpret_cast<uintptr_t>(dsrc) % 8 == 0) && (c->W % 4 == 0) &&
+                           c->centred_exact;
         const int var = variant(c) * 4 + (c->fast ? 2 : 0) + (aligned ? 1 : 0);
         const long long items = (long long)iters * n_pairs * nb;
         long long grid = (long long)c->n_cu * c->icp_blocks_per_cu[var] / c->share;
@@ -3113,6 +3117,24 @@ static FastK fast_consts(const youth_intrinsics& K)
     hl(K.fy, F.hfy, F.lfy);
     hl(K.depth_scale, F.hds, F.lds);
     return F;
+}
+
+// Whether k_icp's aligned pixel loop may form a lane's centred column
+// coordinates by additions: ((float)(u & ~3) - cx) + (u & 3) must equal the
+// spec's (float)u - cx for every column.  It does when cx is near the frame's
+// centre (the difference then keeps cx's ulp); a principal point far to one
+// side (e.g. cx = 20.9316 at W = 640: 9 columns) can make the difference
+// round, and such intrinsics take the unaligned loop, which converts every
+// column (tests/test_gpu_reduce.py::test_off_centre_principal_point).
+static bool centred_exact(float cx, int W)
+{
+    for (int u = 0; u < W; ++u) {
+        volatile float a = (float)u - cx;
+        volatile float b0 = (float)(u & ~3) - cx;
+        volatile float b = b0 + (float)(u & 3);
+        if (a != b) return false;
+    }
+    return true;
 }
 
 // Decide the division path for these intrinsics (k_verify_fastdiv).
@@ -3280,6 +3302,7 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
     const youth_intrinsics Kd = K ? *K : youth_default_intrinsics(W, H);
     c->K = Intr{Kd.fx, Kd.fy, Kd.cx, Kd.cy, Kd.depth_scale};
     c->F = fast_consts(Kd);
+    c->centred_exact = centred_exact(Kd.cx, W);
     c->prm = P ? *P : youth_default_params();
     auto fail = [&](const char* what, hipError_t e) -> youth_icp_ctx* {
         set_error(YOUTH_EHIP, "youth_icp_create: %s (%d)", what, (int)e);

@@ -164,3 +164,44 @@ def test_oracle_reduction_restored():
     with oracle.reduction("lane32", (youth_icp.LANES_STRIDED, 2048, 256, 0)):
         assert oracle.get_reduce() == oracle.REDUCE_LANE32
     assert oracle.get_reduce() == oracle.REDUCE_EXACT
+
+
+def test_off_centre_principal_point(monkeypatch):
+    """k_icp's aligned pixel loop forms a lane's centred columns as
+    ((float)u0 - cx) + q, which equals the spec's (float)u - cx only while the
+    difference keeps cx's ulp.  For a principal point far to one side (cx =
+    20.9316 at W = 640: 9 columns round differently) the context takes the
+    unaligned loop instead: per-iteration counts equal to the oracle's and
+    poses within 1e-9 of it, on the persistent kernel and the stage kernel."""
+    W, H, n, iters = 640, 480, 4, 10
+    cols = np.arange(W)
+    cx = np.float32(20.9316)
+    assert ((np.float32(cols) - cx) != ((np.float32(cols & ~3) - cx) + np.float32(cols & 3))).any()
+    monkeypatch.setenv("YOUTH_ICP_NO_COOP", "1")
+    src, dst, _ = youth_synth.pairs(91, n, W, H)
+    K = youth_icp.default_intrinsics(W, H)
+    K.cx = float(cx)
+    Ko = oracle.viewer_K(W, H)
+    Ko.cx = float(cx)
+    ds, dd = torch.from_numpy(src).cuda(), torch.from_numpy(dst).cuda()
+    torch.cuda.synchronize()
+    with youth_icp.IcpContext(W, H, n, K=K, iters=iters) as ctx:
+        ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), n)
+        ctx.sync()
+        T64, _, st = ctx.get_poses(n)
+        cnt, _ = ctx.get_stats(n, iters)
+        lanes = lanes_of(ctx)
+        T32 = np.asarray(T64[0], np.float32)[:3]
+        g_idx, g_neq = ctx.reduce(src[0], dst[0], T32)
+        rl = ctx.lanes()
+    with oracle_like(lanes):
+        To, sto, stats = oracle.align_batch(src, dst, K=Ko, iters=iters, n_threads=n,
+                                            want_stats=True)
+    assert np.array_equal(st, sto) and not st.any()
+    assert np.array_equal(cnt, stats[..., 0]), np.argwhere(cnt != stats[..., 0])[:4]
+    assert _err(T64, To) <= SAME_VARIANT_TOL, _err(T64, To)
+    assert np.array_equal(g_idx, oracle.associate(src[0], dst[0], T32, Ko))
+    with oracle_like(rl):
+        o_neq = oracle.reduce(src[0], dst[0], T32, Ko)
+    assert g_neq[28] == o_neq[28]
+    np.testing.assert_allclose(g_neq, o_neq, rtol=1e-11, atol=1e-9)
