@@ -367,6 +367,11 @@ def roofline_icp(a, kt, n_pairs, W, H, concurrent=1):
     return out
 
 
+# best 16-B/px non-temporal write stream over 512 x 640 x 480 px measured on
+# an MI355X (tools/hbm_write_bw: 0.426 ms for 2.52 GB; 65536 x 512 threads)
+WRITE_STREAM_CEILING_GBS = 5903.0
+
+
 def roofline_prep(a, kt, n_frames, W, H):
     """k_prep (target records, once per align): 2 B depth in + 16 B record out
     per target pixel, HIP events over a short pass after the timed region.
@@ -389,7 +394,13 @@ def roofline_prep(a, kt, n_frames, W, H):
         traffic = tj["k_prep_bytes_per_px"] * px
         out.update({"traffic": traffic, "traffic_source": src,
                     "traffic_frac": traffic / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                    "traffic_over_algorithmic": traffic / alg})
+                    "traffic_over_algorithmic": traffic / alg,
+                    # 16 of the 18 B/px are writes: against the measured
+                    # ceiling of a pure 16-B/px non-temporal write stream
+                    "write_stream_ceiling": {
+                        "value": WRITE_STREAM_CEILING_GBS, "unit": "GB/s",
+                        "source": "profiles/r04/hbm_write_bw_r4u.txt (tools/hbm_write_bw)",
+                        "traffic_frac": traffic / (avg * 1e-3) / 1e9 / WRITE_STREAM_CEILING_GBS}})
     if tj and "k_prep_valu_busy_frac" in tj:
         acc = tj["k_prep_valu_account"]
         out["valu_issue_frac"] = tj["k_prep_valu_busy_frac"]
