@@ -310,6 +310,14 @@ KNOCKOUTS = {
 }
 
 
+# best 16-B/px non-temporal write stream over 512 x 640 x 480 px measured on
+# an MI355X (tools/hbm_write_bw: 0.426 ms for 2.52 GB; 65536 x 512 threads)
+WRITE_STREAM_CEILING_GBS = 5903.0
+# best 16-B-per-lane streaming read of the same 2.52 GB (0.389 ms; 65536 x 512,
+# profiles/r04/hbm_bw_r4w.txt): what a pure read stream reaches on this GPU
+READ_STREAM_CEILING_GBS = 6476.0
+
+
 def roofline_icp(a, kt, n_pairs, W, H, concurrent=1):
     """Roofline of the dominant kernel, k_icp (persistent: all iterations of
     an align in ONE launch).  `achieved` = the kernel's algorithmic bytes
@@ -346,6 +354,11 @@ def roofline_icp(a, kt, n_pairs, W, H, concurrent=1):
     if traffic is not None:
         out["traffic_frac"] = traffic / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS
         out["traffic_over_algorithmic"] = traffic / alg
+        # k_icp's bytes are reads: against the measured streaming-read ceiling
+        out["read_stream_ceiling"] = {
+            "value": READ_STREAM_CEILING_GBS, "unit": "GB/s",
+            "source": "profiles/r04/hbm_bw_r4w.txt (tools/hbm_write_bw read16)",
+            "traffic_frac": traffic / (avg * 1e-3) / 1e9 / READ_STREAM_CEILING_GBS}
     # what bounds k_icp, from same-box knockout timings: the
     # share of the kernel's time each instruction group accounts for when it
     # is removed.  The PMC issue account (below, "valu") is an upper estimate
@@ -367,9 +380,6 @@ def roofline_icp(a, kt, n_pairs, W, H, concurrent=1):
     return out
 
 
-# best 16-B/px non-temporal write stream over 512 x 640 x 480 px measured on
-# an MI355X (tools/hbm_write_bw: 0.426 ms for 2.52 GB; 65536 x 512 threads)
-WRITE_STREAM_CEILING_GBS = 5903.0
 
 
 def roofline_prep(a, kt, n_frames, W, H):

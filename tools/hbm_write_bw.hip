@@ -4,6 +4,8 @@
 // workgroups):
 //   write16   16 B/px of non-temporal stores, no reads;
 //   write16p  the same with plain stores;
+//   read16    16 B/px of loads over the 2.52 GB record buffer (the read
+//             ceiling k_icp's 18 B/px-iteration stream is measured against);
 //   read2     2 B/px of loads (8 B per lane: 4 px), summed so nothing is dead;
 //   mix       read 2 B + write 16 B per px (k_prep's bytes, no arithmetic),
 //             one lane-contiguous store per px.
@@ -49,6 +51,16 @@ __global__ void k_mix(const short4* in, u4v* out, int n4)
     }
 }
 
+__global__ void k_read16(const u4v* in, long long n, unsigned* sink)
+{
+    unsigned acc = 0;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const u4v v = in[i];
+        acc += v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
 __global__ void k_mix2(const short* in, u4v* out, long long n)
 {
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
@@ -86,6 +98,14 @@ int main()
         for (int grid : {1024, 4096, 16384, 65536}) {
             snprintf(name, sizeof name, "write16 g%d b%d", grid, blk);
             run(name, px * 16.0, [&] { hipLaunchKernelGGL(k_write16, dim3(grid), dim3(blk), 0, 0, (u4v*)out, px, 1); });
+        }
+    }
+    // the read side: 16-B loads over the same 2.52 GB (the records buffer),
+    // several shapes (k_icp streams 18 B/px-iteration of reads)
+    for (int blk : {256, 512}) {
+        for (int grid : {1024, 4096, 16384, 65536}) {
+            snprintf(name, sizeof name, "read16 g%d b%d", grid, blk);
+            run(name, px * 16.0, [&] { hipLaunchKernelGGL(k_read16, dim3(grid), dim3(blk), 0, 0, (const u4v*)out, px, sink); });
         }
     }
     run("write16p", px * 16.0, [&] { hipLaunchKernelGGL(k_write16, dim3(16384), dim3(256), 0, 0, (u4v*)out, px, 0); });
