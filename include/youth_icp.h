@@ -381,6 +381,8 @@ int youth_icp_track_frame(youth_icp_ctx* ctx, const int16_t* depth,
  * submitted frame and returns exactly what youth_icp_track_frame would have
  * returned for it (status bits or a negative code, T_rel, *has_ref).
  * youth_icp_track_frame = submit + collect, with nothing in flight.
+ * collect polls the frame's completion event for up to 2 ms, then blocks in
+ * the runtime (YOUTH_ICP_TRACK_WAIT=sync: block at once).
  * Each frame in flight pins one staging frame of host memory (W x H x 2
  * bytes: 614 KB at 640x480), allocated the first time the ring needs that
  * many and freed by youth_icp_destroy. */
