@@ -74,3 +74,62 @@ def test_align_from_random_initial_poses_both_paths():
             T1, _, s1 = ctx.get_poses(1)
             assert ctx.get_plan()["kernel"] == "k_icp_coop"
             assert s1[0] == want[p][2] and _pose_err(T1[0], want[p][0]) <= POSE_TOL, p
+
+
+def _rand_intrinsics(rng, W, H):
+    """Intrinsics away from the viewer's defaults: focal lengths 300-900 px
+    with fractional parts, a principal point anywhere in the middle 80 % of
+    the frame (off-centre ones exercise the aligned loop's exactness guard),
+    depth scale 1000 / 5000 / 1000.5 (the fast-division verification decides
+    per context)."""
+    return dict(fx=float(np.float32(rng.uniform(300, 900))), fy=float(np.float32(rng.uniform(300, 900))),
+                cx=float(np.float32(rng.uniform(0.1, 0.9) * W)),
+                cy=float(np.float32(rng.uniform(0.1, 0.9) * H)),
+                ds=float(rng.choice([1000.0, 5000.0, 1000.5])))
+
+
+@pytest.mark.parametrize("W,H", [(640, 480), (162, 122)])
+def test_random_intrinsics_every_path(W, H, monkeypatch):
+    """Random intrinsics (6 draws per size; 162 x 122 has W % 4 == 2, the
+    unaligned loops): the stage kernel's association bit-exact and its sums
+    within rel 1e-11 of the oracle in the same reduction; full aligns through
+    the persistent kernel (4 pairs) and k_icp_coop (1 pair) with per-iteration
+    counts equal to the oracle's and poses within 1e-9 of it."""
+    rng = np.random.default_rng(0x1F0C + W)
+    src, dst, _ = youth_synth.pairs(95, 4, W, H)
+    ds, dd = torch.from_numpy(src).cuda(), torch.from_numpy(dst).cuda()
+    torch.cuda.synchronize()
+    iters = 6
+    for draw in range(6):
+        k = _rand_intrinsics(rng, W, H)
+        K = youth_icp.default_intrinsics(W, H)
+        Ko = oracle.viewer_K(W, H)
+        for obj in (K, Ko):
+            obj.fx, obj.fy, obj.cx, obj.cy, obj.depth_scale = k["fx"], k["fy"], k["cx"], k["cy"], k["ds"]
+        T32 = _pose(rng, 2.0, 0.02)[:3].astype(np.float32)
+        with youth_icp.IcpContext(W, H, 4, K=K) as ctx:
+            g_idx, g_neq = ctx.reduce(src[0], dst[0], T32)
+            with oracle_like(ctx):
+                o_neq = oracle.reduce(src[0], dst[0], T32, Ko)
+        assert np.array_equal(g_idx, oracle.associate(src[0], dst[0], T32, Ko)), (draw, k)
+        assert g_neq[28] == o_neq[28], (draw, k)
+        np.testing.assert_allclose(g_neq, o_neq, rtol=1e-11, atol=1e-9, err_msg=str((draw, k)))
+        for n, env in ((4, "1"), (1, None)):
+            if env:
+                monkeypatch.setenv("YOUTH_ICP_NO_COOP", env)
+            else:
+                monkeypatch.delenv("YOUTH_ICP_NO_COOP", raising=False)
+            with youth_icp.IcpContext(W, H, max(n, 2), K=K, iters=iters) as ctx:
+                ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), n)
+                ctx.sync()
+                T64, _, st = ctx.get_poses(n)
+                cnt, _ = ctx.get_stats(n, iters)
+                plan = ctx.get_plan()
+                with oracle_like(ctx):
+                    To, sto, stats = oracle.align_batch(src[:n], dst[:n], K=Ko, iters=iters,
+                                                        n_threads=n, want_stats=True)
+            assert np.array_equal(st, sto), (draw, k, plan["kernel"])
+            assert np.array_equal(cnt, stats[..., 0]), (draw, k, plan["kernel"],
+                                                        np.argwhere(cnt != stats[..., 0])[:4])
+            err = float(np.abs(np.asarray(T64)[..., :3, :4] - np.asarray(To)[..., :3, :4]).max())
+            assert err <= 1e-9, (draw, k, plan["kernel"], err)
