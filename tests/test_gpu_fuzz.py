@@ -133,3 +133,47 @@ def test_random_intrinsics_every_path(W, H, monkeypatch):
                                                         np.argwhere(cnt != stats[..., 0])[:4])
             err = float(np.abs(np.asarray(T64)[..., :3, :4] - np.asarray(To)[..., :3, :4]).max())
             assert err <= 1e-9, (draw, k, plan["kernel"], err)
+
+
+@pytest.mark.parametrize("W,H", [(4, 3), (5, 4), (8, 8), (31, 7), (65, 3), (3, 65), (130, 66)])
+def test_tiny_and_ragged_frames_every_path(W, H, monkeypatch):
+    """Frames down to 4 x 3 and single-tile-row / single-column shapes (the
+    prep tiles, the halo's edge words and the lane partitions all clipped):
+    the stage kernel's association bit-exact and sums within rel 1e-11 of the
+    oracle; full aligns through the persistent kernel (2 pairs) and
+    k_icp_coop (1 pair) with equal per-iteration counts and statuses, poses
+    within 1e-9."""
+    rng = np.random.default_rng(0x7111 + W * 131 + H)
+    src, dst, _ = youth_synth.pairs(96, 2, W, H)
+    ds, dd = torch.from_numpy(src).cuda(), torch.from_numpy(dst).cuda()
+    torch.cuda.synchronize()
+    Ko = oracle.viewer_K(W, H)
+    iters = 5
+    T32 = _pose(rng, 1.0, 0.01)[:3].astype(np.float32)
+    with youth_icp.IcpContext(W, H, 2) as ctx:
+        g_idx, g_neq = ctx.reduce(src[0], dst[0], T32)
+        with oracle_like(ctx):
+            o_neq = oracle.reduce(src[0], dst[0], T32, Ko)
+    assert np.array_equal(g_idx, oracle.associate(src[0], dst[0], T32, Ko))
+    assert g_neq[28] == o_neq[28]
+    np.testing.assert_allclose(g_neq, o_neq, rtol=1e-11, atol=1e-9)
+    for n, env in ((2, "1"), (1, None)):
+        if env:
+            monkeypatch.setenv("YOUTH_ICP_NO_COOP", env)
+        else:
+            monkeypatch.delenv("YOUTH_ICP_NO_COOP", raising=False)
+        with youth_icp.IcpContext(W, H, 2, iters=iters) as ctx:
+            ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), n)
+            ctx.sync()
+            T64, _, st = ctx.get_poses(n)
+            cnt, _ = ctx.get_stats(n, iters)
+            plan = ctx.get_plan()
+            with oracle_like(ctx):
+                To, sto, stats = oracle.align_batch(src[:n], dst[:n], K=Ko, iters=iters,
+                                                    n_threads=n, want_stats=True)
+        assert np.array_equal(st, sto), (plan["kernel"], st, sto)
+        assert np.array_equal(cnt, stats[..., 0]), (plan["kernel"], cnt, stats[..., 0])
+        ok = st == 0
+        if ok.any():
+            err = float(np.abs(np.asarray(T64)[ok][..., :3, :4] - np.asarray(To)[ok][..., :3, :4]).max())
+            assert err <= 1e-9, (plan["kernel"], err)
