@@ -542,8 +542,9 @@ __device__ __forceinline__ void prep_tile(const int16_t* __restrict__ dep, float
         // edge columns x0 - 1 and x0 + kTW one pixel per lane.  An outside
         // pixel back-projects d = 0 at its own (u, v), as before.
         // Words load through a buffer descriptor over the frame: a row
-        // outside the image or a word past the right edge takes offset -1,
-        // which the descriptor's range check returns as 0 (no branch, no
+        // outside the image or a word past the right edge takes the offset
+        // W H 2 (the descriptor's size: past it, with no 32-bit wrap of
+        // offset + bytes), which the range check returns as 0 (no branch, no
         // 64-bit address arithmetic).  The edge pixels are loaded first, so
         // their latency overlaps the words' instead of adding a round trip
         // before the barrier.
@@ -555,7 +556,7 @@ __device__ __forceinline__ void prep_tile(const int16_t* __restrict__ dep, float
             const_cast<int16_t*>(dep), (short)0, W * H * (int)sizeof(int16_t), 0x00020000);
         const bool ein = edge & ((unsigned)egy < (unsigned)H) & ((unsigned)egx < (unsigned)W);
         unsigned short dedge =
-            __builtin_amdgcn_raw_buffer_load_b16(rdep, ein ? (egy * W + egx) * 2 : -1, 0, 0);
+            __builtin_amdgcn_raw_buffer_load_b16(rdep, ein ? (egy * W + egx) * 2 : W * H * 2, 0, 0);
         // every word of the thread is requested before the first is used
         // (kIt loads in flight: 2 at 128 x 24 by 512 threads)
         constexpr int kWords = kTW / 4;  // 32 at 128: a shift, not a divide
@@ -569,7 +570,7 @@ __device__ __forceinline__ void prep_tile(const int16_t* __restrict__ dep, float
             const int c = x0 + 4 * (e - ly * kWords);
             const bool inside = (e < kLH * kWords) & ((unsigned)gy < (unsigned)H) & (c < W);
             wd[it] = __builtin_bit_cast(
-                short4, __builtin_amdgcn_raw_buffer_load_b64(rdep, inside ? (gy * W + c) * 2 : -1, 0, 0));
+                short4, __builtin_amdgcn_raw_buffer_load_b64(rdep, inside ? (gy * W + c) * 2 : W * H * 2, 0, 0));
         }
         // the loads above stay where they are: each result passes through an
         // empty asm here (the frame pointer is __restrict__, so a memory
