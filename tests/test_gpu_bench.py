@@ -53,7 +53,15 @@ def test_bench_single_gpu_contract():
     rp = d["roofline_prep"]
     assert rp["kernel"] == "k_prep" and 0 < rp["frac"] < 1.0
     if rp.get("traffic_source", "").startswith("profiles/"):    # PMC pass of this source
-        assert 1.0 <= rp["traffic_over_algorithmic"] < 1.5 and 0 < rp["valu_issue_frac"] < 1.0
+        assert 1.0 <= rp["traffic_over_algorithmic"] < 1.5
+        wc = rp["write_stream_ceiling"]               # 16 of its 18 B/px are writes
+        assert wc["unit"] == "GB/s" and 0 < wc["traffic_frac"] < 1.2
+        if "valu_issue_frac" in rp:                   # reported, not the limiter evidence
+            assert 0 < rp["valu_issue_frac"] < 1.5
+    if str(rf.get("traffic_source", "")).startswith("profiles/"):
+        assert 1.0 <= rf["traffic_over_algorithmic"] < 1.1
+        rc = rf["read_stream_ceiling"]                # k_icp's bytes are reads
+        assert rc["unit"] == "GB/s" and 0 < rc["traffic_frac"] < 1.2
     cb = d["cpu_baseline"]
     for k in ("value", "unit", "cores", "kind", "sample", "threads_share", "threads_all"):
         assert k in cb, k
