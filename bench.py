@@ -152,10 +152,10 @@ def parse():
                          "as worded (the default), fma = the opt-in fma-chain form; the oracle "
                          "checks in the same spec")
     ap.add_argument("--reduce", choices=["lane32", "exact"],
-                    default=os.environ.get("YOUTH_ICP_REDUCE", "lane32"),
-                    help="spec a9's reduction (youth_icp_set_reduce): lane32 = SURVEY.md §8a a9 as "
-                         "worded, fp32 lane sums -> fp64 finalize (the default); exact = every "
-                         "product exact in fp64 (opt-in)")
+                    default=os.environ.get("YOUTH_ICP_REDUCE", "exact"),
+                    help="spec a9's reduction (youth_icp_set_reduce): exact = every product exact "
+                         "in fp64, launch-independent (the default); lane32 = fp32 lane sums -> "
+                         "fp64 finalize (opt-in: depends on the launch's lane partition)")
     ap.add_argument("--no-spec-parity", action="store_true",
                     help="skip the spec-parity leg (rank 0, N=1)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -297,15 +297,15 @@ def load_pmc(a, W, H):
 
 # Same-box knockout timings of k_icp: the share of the kernel's time each
 # instruction group accounts for when it is removed (timing-only builds, wrong
-# sums).  The default lane32 reduction's update (28 fp32 FMAs per pixel) is
-# 2.2-2.8 % of k_icp (profiles/r04/ab_r4a.txt: 4724 -> 4622 us, 4699 -> 4569
-# us); the exact form's fp64 update was 16 % (profiles/r03/ab_knockout.txt),
-# next to the 32 % the issue account priced it at.
+# sums).  The exact reduction's fp64 update (the default) was 16 % of k_icp
+# (profiles/r03/ab_knockout.txt), next to the 32 % the issue account priced
+# it at; the opt-in lane32 form's update (28 fp32 FMAs per pixel) is 2.2-2.8 %
+# (profiles/r04/ab_r4a.txt: 4724 -> 4622 us, 4699 -> 4569 us).
 KNOCKOUTS = {
-    "source": "profiles/r04/ab_r4a.txt (lane32), profiles/r03/ab_knockout.txt (exact)",
-    "lane32_fp32_update": {"measured_time_share": 0.025, "reduction": "lane32 (default)"},
+    "source": "profiles/r03/ab_knockout.txt (exact), profiles/r04/ab_r4a.txt (lane32)",
     "exact_fp64_update": {"measured_time_share": 0.16, "issue_account_share": 0.32,
-                          "reduction": "exact (opt-in)"},
+                          "reduction": "exact (default)"},
+    "lane32_fp32_update": {"measured_time_share": 0.025, "reduction": "lane32 (opt-in)"},
     "target_int_to_float": {"measured_time_share": 0.005, "issue_account_share": 0.033},
 }
 
@@ -418,6 +418,35 @@ def roofline_prep(a, kt, n_frames, W, H):
     return out
 
 
+def parity_sample(n):
+    """Shard positions every rank checks against the CPU oracle after the
+    timed region: its first two and last two pairs."""
+    return sorted({i for i in (0, 1, n - 2, n - 1) if 0 <= i < n})
+
+
+def shard_parity(a, src, dst, T, idx):
+    """max |T - T_cpu| over the pairs `idx` of this rank's shard (src[i] is
+    aligned onto dst[i]; T the GPU's fp64 poses), the C oracle in the exact
+    reduction, a few threads per rank."""
+    if not idx:
+        return 0.0
+    oracle = oracle_mod()
+    idx = np.asarray(idx)
+    T_cpu, _ = oracle.align_batch(np.ascontiguousarray(src[idx]), np.ascontiguousarray(dst[idx]),
+                                  iters=a.iters, n_threads=min(len(idx), 4))
+    return pose_err(np.asarray(T)[idx], T_cpu)
+
+
+def parity_gate(result):
+    """True when every rank's sampled poses are within POSE_TOL of the CPU
+    oracle; stored in the line as `parity_all_ranks_ok` (rank 0 then exits
+    non-zero if False)."""
+    errs = result["ranks"].get("per_rank", {}).get("pose_max_abs_err_vs_cpu", [])
+    ok = bool(errs) and max(errs) <= POSE_TOL
+    result["parity_all_ranks_ok"] = ok
+    return ok
+
+
 def pose_err(Ta, Tb):
     """max |Ta - Tb| over the 3x4 entries (any leading shape)."""
     Ta = np.asarray(Ta, np.float64).reshape(-1, 4, 4)
@@ -523,11 +552,18 @@ def run_pairs(R):
     # (collective: all ranks), so an N > 1 line shows that N ranks ran and
     # splits compute from the collective
     gms = gather_ms(R, poses[0], gathered[0], world, counts, main, side)
+    # every rank checks its shard's first and last two pairs against the CPU
+    # oracle (these pairs sit at the shard's own launch geometry)
+    idx = parity_sample(n)
+    perr = shard_parity(a, src, dst, T_gpu, idx)
     result["ranks"] = youth_dist.rank_report({
         "k_icp_ms": result["kernel_ms_per_step"]["k_icp"],
         "k_prep_ms": result["kernel_ms_per_step"]["k_prep"],
-        "gather_ms": gms if gms is not None else 0.0}, world)
+        "gather_ms": gms if gms is not None else 0.0}, world,
+        {"pose_max_abs_err_vs_cpu": perr, "pairs_checked": len(idx)})
     result["ranks"]["gather_timed"] = gms is not None
+    result["ranks"]["parity_sample"] = "each rank: its shard's first 2 and last 2 pairs vs the C oracle"
+    parity_gate(result)
     if rank == 0 and world == 1:
         leg = {}
         if not a.no_cpu_baseline:
@@ -1014,19 +1050,26 @@ def slam_rate_c(a, n, passes):
     return json.loads(r.stdout.strip().splitlines()[-1])
 
 
-def survey_noise_parity(a, ctx, main, n=16):
+def survey_noise_parity(a, ctx, main, n=128):
     """Parity on SURVEY §8d's noise level (sigma = 1.5 mm Z^2; the bench's
     default synthetic pairs use 0.25 mm Z^2): n pairs through the
-    same context vs the C oracle."""
+    same context (one launch) vs the C oracle in the exact reduction."""
     oracle = oracle_mod()
     src, dst, _ = youth_synth.pairs(0, n, a.width, a.height, flags=youth_synth.SURVEY_FLAGS)
     ds, dd = torch.from_numpy(src).cuda(), torch.from_numpy(dst).cuda()
+    own = ctx.max_frames < n            # a small --global-pairs run: a context of n pairs
+    if own:
+        ctx = youth_icp.IcpContext(a.width, a.height, n, iters=a.iters)
     ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), n, stream=main.cuda_stream)
     T, _, st = ctx.get_poses(n)
+    if own:
+        ctx.close()
     T_cpu, st_cpu = oracle.align_batch(src, dst, iters=a.iters, n_threads=min(n, _cpus()))
+    err = np.abs(np.asarray(T)[:, :3, :] - np.asarray(T_cpu)[:, :3, :]).reshape(n, -1).max(1)
     return {"pairs": n, "noise": "sigma = 1.5 mm * Z^2", "pose_max_abs_err_vs_cpu":
-            pose_err(T, T_cpu), "status_gpu": [int(v) for v in st],
-            "status_cpu": [int(v) for v in st_cpu]}
+            float(err.max()), "pairs_over_tol": int((err > POSE_TOL).sum()),
+            "status_gpu_nonzero": int((st != 0).sum()),
+            "status_cpu_nonzero": int((st_cpu != 0).sum())}
 
 
 def viewer_cloud_rate(R, d_depth, depth_host, reps=20, warmup=3):
@@ -1127,11 +1170,19 @@ def run_sequence(R):
             torch.cuda.synchronize()
             ts.append((time.perf_counter() - t0) * 1e3)
         g_ms = float(np.median(ts))
+    # every rank checks its first pair and its halo pair (the last, whose
+    # source frame is the next shard's first) against the CPU oracle
+    idx = sorted({0, npairs - 1}) if npairs else []
+    T_rel = ctx.get_poses(npairs)[0] if npairs else None
+    perr = shard_parity(a, frames[1:], frames[:-1], T_rel, idx)
     result["ranks"] = youth_dist.rank_report({
         "k_icp_ms": kt["k_icp"][0] / max(kt["k_icp"][1], 1),
         "k_prep_ms": kt["k_prep"][0] / max(kt["prep_pass_steps"], 1),
-        "gather_ms": g_ms if g_ms is not None else 0.0}, world)
+        "gather_ms": g_ms if g_ms is not None else 0.0}, world,
+        {"pose_max_abs_err_vs_cpu": perr, "pairs_checked": len(idx)})
     result["ranks"]["gather_timed"] = g_ms is not None
+    result["ranks"]["parity_sample"] = "each rank: its first pair and its halo pair vs the C oracle"
+    parity_gate(result)
     if rank == 0:
         T = youth_dist.compose_trajectory(traj["T"].cpu().numpy().reshape(-1, 4, 4))
         result["trajectory_frames"] = int(T.shape[0])
@@ -1160,9 +1211,10 @@ def base_result(R, value, elapsed):
                            if a.spec == "survey" else
                            "fma chains, one correctly rounded reciprocal (opt-in)"),
                  "a9_reduce": a.reduce,
-                 "a9": ("SURVEY.md §8a a9 as worded: fp32 lane sums (one fma each), fp64 finalize"
-                        if a.reduce == "lane32" else
-                        "every product exact in fp64 (opt-in)")},
+                 "a9": ("every product exact in fp64, fp64 sums (launch-independent; the default)"
+                        if a.reduce == "exact" else
+                        "fp32 lane sums (one fma each), fp64 finalize (opt-in; depends on the "
+                        "launch's lane partition)")},
         "data": "synthetic (ray-cast room scene, int16 mm depth, seeds 0x5EED0000+pair / "
                 "0x5EED1000 sequence)",
     }
@@ -1259,6 +1311,10 @@ def main():
     if R.rank == 0:
         print(json.dumps(result), flush=True)
     R.finish()
+    if R.rank == 0 and not result.get("parity_all_ranks_ok", True):
+        sys.stderr.write("bench.py: a rank's poses are more than %g from the CPU oracle: %s\n"
+                         % (POSE_TOL, result["ranks"].get("per_rank")))
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -150,18 +150,28 @@ int youth_icp_set_spec(youth_icp_ctx* ctx, int spec);
 int youth_icp_get_spec(const youth_icp_ctx* ctx);
 
 /* Reduction of spec a9 (the 28 sums of J J^T, J r, r^2):
- *   YOUTH_REDUCE_LANE32 (default) SURVEY.md §8a a9 as worded, "fp32 lanes ->
- *                     fp64 finalize": each GPU lane sums its matched pixels'
- *                     28 products with one fp32 fma each over its whole share
- *                     of an iteration, converts them to fp64 once, and the
- *                     lanes are added in fp64 (fixed order);
- *   YOUTH_REDUCE_EXACT opt-in: every product of two fp32 values exact in fp64
- *                     (one fp64 fma per product), ~10 % slower k_icp.
+ *   YOUTH_REDUCE_EXACT (default) every product of two fp32 values exact in
+ *                     fp64 (one fp64 fma per product), accumulated in fp64.
+ *                     Launch-independent: the same pair aligned in any batch
+ *                     size, shard, chunking or kernel path gives the same pose
+ *                     up to fp64 summation order (~1e-16 relative), within
+ *                     1e-5 of the CPU oracle at SURVEY §8d noise;
+ *   YOUTH_REDUCE_LANE32 opt-in: each GPU lane sums its matched pixels' 28
+ *                     products with one fp32 fma each over its whole share of
+ *                     an iteration, converts them to fp64 once, and the lanes
+ *                     are added in fp64 (fixed order); ~10 % faster k_icp.
+ *                     Its results depend on the launch's lane partition (pairs
+ *                     per launch, chunking, shard count, YOUTH_ICP_BATCH_CHUNK,
+ *                     persistent vs cooperative kernel): they are
+ *                     bit-reproducible only for the same launch shape, and
+ *                     at SURVEY §8d noise a pose can move by up to ~5e-5.
  * youth_icp_set_reduce returns the previous mode (EINVAL for another value);
  * the environment YOUTH_ICP_REDUCE=lane32|exact sets a new context's initial
  * mode.  youth_icp_get_lanes reports how the last align partitioned each
  * iteration's source pixels into lanes (the oracle's oracle_set_reduce
- * restates a LANE32 iteration exactly given that partition):
+ * restates a LANE32 iteration exactly given that partition); it returns
+ * YOUTH_EINVAL when the last call ran launches of more than one partition
+ * (a pipelined youth_icp_align_batch whose chunks took different kernels):
  *   YOUTH_LANES_STRIDED   workgroups of `threads` lanes own chunks of `chunk`
  *                         pixels; in each step of 4 threads pixels, lane l
  *                         takes pixels 4l .. 4l+3 (k_icp, k_reduce);
@@ -501,6 +511,28 @@ long long youth_slam_batched_frames(void);
 int youth_slam_queue_size(void);
 /* Block until the module stops (used by algorithmModule). */
 void youth_slam_wait_stopped(void);
+
+/* Event trace of the ingest path (diagnostic, additive): with a capacity > 0
+ * the producer (processSlamFrame) and the worker record timestamped events
+ * (CLOCK_MONOTONIC seconds, the clock rocprofv3 traces use) into a
+ * fixed-size buffer, lock-free; events past the capacity are dropped.
+ * youth_slam_trace_enable(0) stops recording and frees the buffer.  Enable
+ * or disable only while no frame is being pushed.  youth_slam_trace_read
+ * copies up to n events (t[n] seconds, kind[n], arg[n]) and returns how many
+ * were recorded (may exceed n).  Kinds and their arg: */
+#define YOUTH_SLAM_EV_PUSH_BEGIN    1  /* queue depth before the push */
+#define YOUTH_SLAM_EV_PUSH_END      2  /* buffer: 0 pooled, 1 new page-locked, 2 new pageable */
+#define YOUTH_SLAM_EV_TAKE          3  /* frames in the micro-batch being formed */
+#define YOUTH_SLAM_EV_SUBMIT_BEGIN  4  /* frames submitted */
+#define YOUTH_SLAM_EV_SUBMIT_END    5  /* return code */
+#define YOUTH_SLAM_EV_COLLECT_BEGIN 6  /* frames in flight */
+#define YOUTH_SLAM_EV_COLLECT_END   7  /* 1 the last frame of its submission */
+#define YOUTH_SLAM_EV_IDLE_BEGIN    8  /* worker waits for a frame (queue empty) */
+#define YOUTH_SLAM_EV_IDLE_END      9  /* queue depth */
+#define YOUTH_SLAM_EV_POOL          10 /* worker: page-locked buffers allocated (+) / freed (-) */
+#define YOUTH_SLAM_EV_DROP          11 /* frames dropped by the >10 -> 5 policy */
+int youth_slam_trace_enable(int capacity);
+int youth_slam_trace_read(int n, double* t, int* kind, int* arg);
 
 #ifdef __cplusplus
 }

@@ -532,6 +532,11 @@ __device__ __forceinline__ void prep_tile(const int16_t* __restrict__ dep, float
     constexpr int kLH = kTH + 2;
     constexpr int kLW = kTW + 2;
     static_assert(kTW % 64 == 0 && kThreads % kTW == 0, "rows of whole waves");
+    // the record loop below covers kTH rows in steps of kThreads / kTW: a
+    // tile height that is not a multiple would leave its bottom rows unwritten
+    static_assert(kTH % (kThreads / kTW) == 0, "tile rows a multiple of the rows per step");
+    // the three LDS planes of the halo'd tile must fit a workgroup's 160 KB
+    static_assert(3 * (kTH + 2) * (kTW + 2) * sizeof(float) <= 160 * 1024, "LDS planes fit");
     const int tx = threadIdx.x % kTW;
     const int ty = threadIdx.x / kTW;
     if (kWide) {
@@ -2471,9 +2476,10 @@ struct youth_icp_ctx {
     unsigned* d_epoch = nullptr;     // [max_frames] persistent pose epochs
     unsigned* d_head = nullptr;      // queue words kQHead / kQError / kQSpins / kQWaited
     bool persistent = true;          // one k_icp launch per align (else per-iteration k_reduce)
-    int reduce = YOUTH_REDUCE_LANE32; // spec a9 (youth_icp_set_reduce, YOUTH_ICP_REDUCE)
+    int reduce = YOUTH_REDUCE_EXACT; // spec a9 (youth_icp_set_reduce, YOUTH_ICP_REDUCE)
     youth_lanes lanes{};             // lane partition of the last align's iterations
     bool has_lanes = false;
+    bool lanes_mixed = false;        // the last host batch call ran more than one partition
     int icp_blocks_per_cu[4 * kVariants] = {};  // occupancy of k_icp<variant, fast, aligned> [variant 4 + fast 2 + aligned]
     int n_cu = 0;
     // small batches: k_icp_coop (youth_icp_create reads the knobs)
@@ -2745,6 +2751,7 @@ static int launch_reduce(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, P
     HIP_TRY(hipGetLastError());
     c->lanes = youth_lanes{YOUTH_LANES_STRIDED, chunk, kRedThreads, 0};
     c->has_lanes = true;
+    c->lanes_mixed = false;
     *nblk_out = nb;
     return ev_end(c, s, &ep);
 }
@@ -2942,6 +2949,7 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
     c->lanes = youth_lanes{tile_src ? YOUTH_LANES_COOP_TILE : YOUTH_LANES_COOP, npx * c->coop_threads,
                            c->coop_threads, npx};
     c->has_lanes = true;
+    c->lanes_mixed = false;
     return ev_end(c, s, &ep);
 }
 
@@ -3068,6 +3076,7 @@ static int run_iterations(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, 
         HIP_TRY(hipGetLastError());
         c->lanes = youth_lanes{YOUTH_LANES_STRIDED, chunk, kRedThreads, 0};
         c->has_lanes = true;
+        c->lanes_mixed = false;
         rc = ev_end(c, s, &ep);
         if (rc) return rc;
     } else {
@@ -3214,6 +3223,9 @@ int youth_icp_get_lanes(const youth_icp_ctx* c, youth_lanes* out)
 {
     if (!c || !out) return set_error(YOUTH_EINVAL, "get_lanes: bad arguments");
     if (!c->has_lanes) return set_error(YOUTH_EINVAL, "get_lanes: no align has run");
+    if (c->lanes_mixed)
+        return set_error(YOUTH_EINVAL, "get_lanes: the last call ran launches of more than one "
+                                       "lane partition");
     *out = c->lanes;
     return YOUTH_OK;
 }
@@ -3809,6 +3821,8 @@ static int batch_on_device(int dev, const int16_t* src, const int16_t* dst, int 
         HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         c->xfer_ev.push_back(e);
     }
+    youth_lanes first_lanes{};
+    bool mixed = false;
     for (int k = 0; k < n_chunks; ++k) {
         const size_t p0 = (size_t)k * chunk;
         const int cnt = (int)std::min<size_t>(chunk, n_pairs - p0);
@@ -3824,6 +3838,12 @@ static int batch_on_device(int dev, const int16_t* src, const int16_t* dst, int 
         rc = youth_icp_align_pairs_device(c, d_s + p0 * N, d_d + p0 * N, cnt, nullptr,
                                           c->d_Tout + p0 * 16, s);
         if (rc) return drain(rc);
+        // a tail chunk may take another kernel (and lane partition) than the
+        // full chunks: youth_icp_get_lanes then reports the call as mixed
+        if (k == 0)
+            first_lanes = c->lanes;
+        else
+            mixed |= memcmp(&first_lanes, &c->lanes, sizeof(youth_lanes)) != 0;
         if (status_out) {
             hipLaunchKernelGGL(k_status_out, dim3((cnt + 255) / 256), dim3(256), 0, s,
                                c->d_status, cnt, (const unsigned*)(c->d_head + kQError),
@@ -3843,6 +3863,7 @@ static int batch_on_device(int dev, const int16_t* src, const int16_t* dst, int 
         if (e != hipSuccess)
             return drain(set_error(YOUTH_EHIP, "align_batch: %s", hipGetErrorString(e)));
     }
+    c->lanes_mixed = mixed;
     hipError_t e = hipMemcpyAsync(T_out, c->d_Tout, (size_t)n_pairs * 16 * sizeof(float),
                                   hipMemcpyDeviceToHost, s);
     if (e == hipSuccess && status_out)

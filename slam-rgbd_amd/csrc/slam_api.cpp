@@ -17,6 +17,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <algorithm>
 #include <atomic>
@@ -25,11 +26,42 @@
 #include <condition_variable>
 #include <deque>
 #include <mutex>
+#include <new>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "youth_icp.h"
+
+// ----------------------------------------------------------- event trace --
+// youth_slam_trace_enable / _read (youth_icp.h): timestamped events of the
+// producer and the worker in a fixed buffer, one fetch_add per event.
+namespace {
+
+struct TraceEv {
+    double t;
+    int kind, arg;
+};
+std::atomic<TraceEv*> g_tr{nullptr};
+std::atomic<int> g_tr_n{0};
+int g_tr_cap = 0;
+
+double mono_s()
+{
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+void trace(int kind, int arg)
+{
+    TraceEv* b = g_tr.load(std::memory_order_acquire);
+    if (!b) return;
+    const int i = g_tr_n.fetch_add(1, std::memory_order_relaxed);
+    if (i < g_tr_cap) b[i] = TraceEv{mono_s(), kind, arg};
+}
+
+}  // namespace
 
 // ------------------------------------------------------- ingest queue -----
 // Frames live in reusable buffers: a push copies the caller's frame into a
@@ -39,6 +71,14 @@
 // kPinnedBytes of them), which the worker takes out of the queue and submits
 // to the tracker in place (youth_icp_track_submit_pinned), returning each to
 // the pool once its frame has been collected.
+// Page-locked buffers are allocated and freed only off the producer's path
+// (initSlamModule and the worker: queue_prefill / queue_release): a
+// hipHostMalloc or hipHostFree can take milliseconds and synchronise the
+// device, which a camera callback must not wait for.  A producer that finds
+// no pooled buffer of the frame's size takes a pageable one (malloc); the
+// worker frees it after use and adds a page-locked one to the pool.  Pooled
+// page-locked buffers are never freed on a full pool: the page-locked budget
+// bounds how many exist.
 struct youth_frame_queue {
     struct Item {
         int16_t* buf = nullptr;
@@ -48,7 +88,7 @@ struct youth_frame_queue {
         uint32_t ts = 0;
     };
     static constexpr size_t kPinnedBytes = (size_t)256 << 20;
-    static constexpr size_t kPoolMax = 48;  // free buffers kept
+    static constexpr size_t kPoolMax = 48;  // pageable buffers kept
     std::mutex mu;
     std::deque<Item> q;
     // q.size(), stored under mu after every change: youth_queue_size reads
@@ -57,8 +97,9 @@ struct youth_frame_queue {
     std::atomic<int> depth{0};
     std::vector<Item> pool;
     int high = 10, low = 5;
-    bool pinned = false;      // allocate page-locked buffers (SLAM module queue)
+    bool pinned = false;      // page-locked buffers (SLAM module queue), allocated off the producer path
     size_t pinned_bytes = 0;  // page-locked bytes allocated and not freed
+    int pinned_count = 0;     // page-locked buffers allocated and not freed
 };
 
 namespace {
@@ -70,6 +111,7 @@ void buf_free(youth_frame_queue* q, youth_frame_queue::Item& it)
         youth_icp_host_free(it.buf);
         std::lock_guard<std::mutex> lk(q->mu);
         q->pinned_bytes -= it.cap * sizeof(int16_t);
+        --q->pinned_count;
     } else {
         free(it.buf);
     }
@@ -77,65 +119,60 @@ void buf_free(youth_frame_queue* q, youth_frame_queue::Item& it)
     it.cap = 0;
 }
 
-bool buf_alloc(youth_frame_queue* q, size_t n, bool want_pinned, youth_frame_queue::Item& it);
-
-// a buffer of >= n values: from the pool, else newly allocated (page-locked
-// while the queue's budget lasts)
-bool buf_get(youth_frame_queue* q, size_t n, youth_frame_queue::Item& it)
+// A buffer of >= n values for the producer: a pooled one, else (no pooled
+// buffer fits, or the queue is not page-locked) a new pageable one.  *kind:
+// 0 pooled, 1 new page-locked, 2 new pageable.  No page-locked allocation on
+// this path when q->pinned (the worker does those).
+bool buf_get(youth_frame_queue* q, size_t n, youth_frame_queue::Item& it, int* kind)
 {
-    youth_frame_queue::Item old;
-    bool want_pinned = false;
     {
         std::lock_guard<std::mutex> lk(q->mu);
-        if (!q->pool.empty()) {
-            old = q->pool.back();
-            q->pool.pop_back();
-            if (old.cap >= n) {
-                it.buf = old.buf;
-                it.cap = old.cap;
-                it.pinned = old.pinned;
-                return true;
-            }
+        for (size_t k = q->pool.size(); k-- > 0;) {
+            if (q->pool[k].cap < n) continue;
+            it.buf = q->pool[k].buf;
+            it.cap = q->pool[k].cap;
+            it.pinned = q->pool[k].pinned;
+            q->pool.erase(q->pool.begin() + (long)k);
+            *kind = 0;
+            return true;
         }
-        want_pinned = q->pinned && q->pinned_bytes + n * sizeof(int16_t) <= q->kPinnedBytes;
-        if (want_pinned) q->pinned_bytes += n * sizeof(int16_t);
     }
-    buf_free(q, old);  // too small for this frame size
-    return buf_alloc(q, n, want_pinned, it);
-}
-
-// a new buffer of n values (page-locked while the queue's budget lasts)
-bool buf_new(youth_frame_queue* q, size_t n, youth_frame_queue::Item& it)
-{
-    bool want_pinned = false;
-    {
-        std::lock_guard<std::mutex> lk(q->mu);
-        want_pinned = q->pinned && q->pinned_bytes + n * sizeof(int16_t) <= q->kPinnedBytes;
-        if (want_pinned) q->pinned_bytes += n * sizeof(int16_t);
-    }
-    return buf_alloc(q, n, want_pinned, it);
-}
-
-// the allocation behind buf_get / buf_new (want_pinned: budget already taken)
-bool buf_alloc(youth_frame_queue* q, size_t n, bool want_pinned, youth_frame_queue::Item& it)
-{
-    it.buf = want_pinned ? youth_icp_host_alloc(n) : nullptr;
-    it.pinned = it.buf != nullptr;
-    if (want_pinned && !it.buf) {
-        std::lock_guard<std::mutex> lk(q->mu);
-        q->pinned_bytes -= n * sizeof(int16_t);
-    }
-    if (!it.buf) it.buf = static_cast<int16_t*>(malloc(n * sizeof(int16_t)));
+    *kind = 2;
+    it.buf = static_cast<int16_t*>(malloc(n * sizeof(int16_t)));
+    it.pinned = false;
     it.cap = it.buf ? n : 0;
     return it.buf != nullptr;
 }
 
-// back to the pool (q->mu held), or freed when the pool is full
+// A new page-locked buffer of n values while the budget lasts (worker / init).
+bool buf_new_pinned(youth_frame_queue* q, size_t n, youth_frame_queue::Item& it)
+{
+    {
+        std::lock_guard<std::mutex> lk(q->mu);
+        if (q->pinned_bytes + n * sizeof(int16_t) > q->kPinnedBytes) return false;
+        q->pinned_bytes += n * sizeof(int16_t);
+        ++q->pinned_count;
+    }
+    it.buf = youth_icp_host_alloc(n);
+    if (!it.buf) {
+        std::lock_guard<std::mutex> lk(q->mu);
+        q->pinned_bytes -= n * sizeof(int16_t);
+        --q->pinned_count;
+        return false;
+    }
+    it.pinned = true;
+    it.cap = n;
+    return true;
+}
+
+// back to the pool (q->mu held): page-locked buffers always (the budget
+// bounds them), pageable ones up to kPoolMax (else freed by the caller, which
+// is plain free())
 void pool_put_locked(youth_frame_queue* q, youth_frame_queue::Item& it,
                      std::vector<youth_frame_queue::Item>& to_free)
 {
     if (!it.buf) return;
-    if (q->pool.size() < q->kPoolMax)
+    if (it.pinned || (!q->pinned && q->pool.size() < q->kPoolMax))
         q->pool.push_back(it);
     else
         to_free.push_back(it);
@@ -159,40 +196,58 @@ int queue_take(youth_frame_queue* q, youth_frame_queue::Item& out)
     return 1;
 }
 
-// Fill the pool with buffers of n values until it holds `count` of them
-// (page-locked while the budget lasts); smaller pooled buffers are freed.
-void queue_prefill(youth_frame_queue* q, size_t n, int count)
+// Page-locked buffers of n values until `count` exist (worker / init; pooled
+// buffers smaller than n are freed first: a resolution change).  Returns the
+// number allocated minus the number freed.
+int queue_prefill(youth_frame_queue* q, size_t n, int count)
 {
-    std::vector<youth_frame_queue::Item> fresh, to_free;
+    std::vector<youth_frame_queue::Item> to_free;
     {
         std::lock_guard<std::mutex> lk(q->mu);
         std::vector<youth_frame_queue::Item> keep;
         for (auto& it : q->pool) (it.cap >= n ? keep : to_free).push_back(it);
         q->pool.swap(keep);
-        count -= (int)q->pool.size();
     }
+    const int freed = (int)to_free.size();
     free_all(q, to_free);
-    for (int i = 0; i < count; ++i) {
-        youth_frame_queue::Item it;
+    int added = 0;
+    for (;;) {
         {
             std::lock_guard<std::mutex> lk(q->mu);
-            if (q->pool.size() + fresh.size() >= q->kPoolMax) break;
+            if (q->pinned_count >= count) break;
         }
-        if (!buf_new(q, n, it)) break;
-        fresh.push_back(it);
+        youth_frame_queue::Item it;
+        if (!buf_new_pinned(q, n, it)) break;
+        std::lock_guard<std::mutex> lk(q->mu);
+        q->pool.push_back(it);
+        ++added;
     }
-    std::lock_guard<std::mutex> lk(q->mu);
-    for (auto& it : fresh) q->pool.push_back(it);
+    return added - freed;
 }
 
-void queue_release(youth_frame_queue* q, youth_frame_queue::Item& it)
+// The worker's pass over a returned buffer: page-locked ones go back to the
+// pool; a pageable one (the producer found the pool empty) is freed and, while
+// fewer than `target` page-locked buffers exist, replaced by a page-locked one
+// of n values.  Returns 1 when it allocated one.
+int queue_release(youth_frame_queue* q, youth_frame_queue::Item& it, size_t n = 0, int target = 0)
 {
+    const bool was_pageable = it.buf && !it.pinned;
     std::vector<youth_frame_queue::Item> to_free;
     {
         std::lock_guard<std::mutex> lk(q->mu);
         pool_put_locked(q, it, to_free);
     }
     free_all(q, to_free);
+    if (!was_pageable || !q->pinned || n == 0) return 0;
+    {
+        std::lock_guard<std::mutex> lk(q->mu);
+        if (q->pinned_count >= target) return 0;
+    }
+    youth_frame_queue::Item fresh;
+    if (!buf_new_pinned(q, n, fresh)) return 0;
+    std::lock_guard<std::mutex> lk(q->mu);
+    q->pool.push_back(fresh);
+    return 1;
 }
 
 }  // namespace
@@ -225,7 +280,9 @@ int youth_queue_push(youth_frame_queue* q, const int16_t* depth, int width, int 
     if (!q || !depth || width <= 0 || height <= 0) return YOUTH_EINVAL;
     const size_t n = (size_t)width * (size_t)height;
     youth_frame_queue::Item it;
-    if (!buf_get(q, n, it)) return YOUTH_ENOMEM;
+    int kind = 0;
+    trace(YOUTH_SLAM_EV_PUSH_BEGIN, youth_queue_size(q));
+    if (!buf_get(q, n, it, &kind)) return YOUTH_ENOMEM;
     memcpy(it.buf, depth, n * sizeof(int16_t));
     it.w = width;
     it.h = height;
@@ -248,6 +305,8 @@ int youth_queue_push(youth_frame_queue* q, const int16_t* depth, int width, int 
         q->depth.store((int)q->q.size(), std::memory_order_release);
     }
     free_all(q, to_free);
+    if (dropped) trace(YOUTH_SLAM_EV_DROP, dropped);
+    trace(YOUTH_SLAM_EV_PUSH_END, kind);
     return dropped;
 }
 
@@ -382,6 +441,16 @@ youth_intrinsics intrinsics_for(int w, int h)
     return youth_default_intrinsics(w, h);
 }
 
+// Frames per micro-batch of the worker (YOUTH_SLAM_TRACK_BATCH, default
+// YOUTH_TRACK_MAX_BATCH) and the page-locked buffers its queue keeps: a
+// backlog holds about queue (11) + in flight (2 batch) + one batch of frames.
+int slam_batch()
+{
+    const char* eb = getenv("YOUTH_SLAM_TRACK_BATCH");
+    return eb ? std::max(1, std::min(atoi(eb), YOUTH_TRACK_MAX_BATCH)) : YOUTH_TRACK_MAX_BATCH;
+}
+int pool_target(int batch) { return 11 + 3 * batch; }
+
 // SLAM.cpp:32-63 processFramesThread, with TrackRGBD replaced by HIP ICP.
 // The worker takes every frame of the current size already queued behind
 // the one it pops, up to `batch` (YOUTH_TRACK_MAX_BATCH by default;
@@ -400,9 +469,7 @@ void worker_main(int device)
     fprintf(stderr, "youth_icp: SLAM processing thread started\n");
     youth_icp_ctx* ctx = nullptr;
     int cw = 0, ch = 0;
-    const char* eb = getenv("YOUTH_SLAM_TRACK_BATCH");
-    const int batch = eb ? std::max(1, std::min(atoi(eb), YOUTH_TRACK_MAX_BATCH))
-                         : YOUTH_TRACK_MAX_BATCH;
+    const int batch = slam_batch();
     std::vector<int16_t> packed;  // pageable frames of a micro-batch, packed (rare)
     bool held = false;            // a taken frame of another size (or sequence), next round
     Item held_item;
@@ -423,8 +490,11 @@ void worker_main(int device)
         subs -= pr0.last;
         double T_rel[16];
         int has_ref = 0;
+        trace(YOUTH_SLAM_EV_COLLECT_BEGIN, (int)pend.size() + 1);
         const int st = youth_icp_track_collect(ctx, T_rel, &has_ref);
-        queue_release(g_queue, pr0.item);
+        trace(YOUTH_SLAM_EV_COLLECT_END, pr0.last ? 1 : 0);
+        if (queue_release(g_queue, pr0.item, (size_t)cw * ch, pool_target(batch)))
+            trace(YOUTH_SLAM_EV_POOL, 1);
         if (st < 0) {
             fprintf(stderr, "youth_icp: tracking failed: %s\n", youth_icp_last_error());
             return;
@@ -468,6 +538,7 @@ void worker_main(int device)
                 continue;
             }
             g_busy.store(false);
+            trace(YOUTH_SLAM_EV_IDLE_BEGIN, 0);
             {
                 // the predicate re-checks the queue under g_wake_mu, which
                 // processSlamFrame takes before notifying: no lost wake-up
@@ -477,6 +548,7 @@ void worker_main(int device)
                 g_wake_cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(20),
                                      [] { return !g_process.load() || youth_queue_size(g_queue) > 0; });
             }
+            trace(YOUTH_SLAM_EV_IDLE_END, youth_queue_size(g_queue));
             continue;
         }
         const int w = items[0].w, h = items[0].h;
@@ -500,9 +572,9 @@ void worker_main(int device)
                 continue;
             }
             if (batch > 1) youth_icp_track_set_batch(ctx, batch);
-            // page-locked buffers for this size up front: a backlog keeps
-            // about queue (11) + in flight (2 batch) + one batch of frames
-            queue_prefill(g_queue, (size_t)w * h, 11 + 3 * batch);
+            // page-locked buffers for this size up front (initSlamModule made
+            // them for the configured size already)
+            trace(YOUTH_SLAM_EV_POOL, queue_prefill(g_queue, (size_t)w * h, pool_target(batch)));
         }
         const size_t N = (size_t)w * h;
         // two submissions in flight: with two queued, finish the oldest
@@ -529,12 +601,14 @@ void worker_main(int device)
                 held = true;
             }
         }
+        trace(YOUTH_SLAM_EV_TAKE, m);
         // the tracker holds 2 batch frames in flight
         while (!pend.empty() && (int)pend.size() + m > 2 * batch) finish_one(true);
         const long long chained0 = youth_icp_track_chained_frames(ctx);
         bool pinned = true;
         for (int i = 0; i < m; ++i) pinned &= items[i].pinned;
         int rc;
+        trace(YOUTH_SLAM_EV_SUBMIT_BEGIN, m);
         if (pinned) {
             const int16_t* fr[YOUTH_TRACK_MAX_BATCH];
             for (int i = 0; i < m; ++i) fr[i] = items[i].buf;
@@ -547,6 +621,7 @@ void worker_main(int device)
                 memcpy(packed.data() + (size_t)i * N, items[i].buf, N * sizeof(int16_t));
             rc = youth_icp_track_submit_batch(ctx, packed.data(), m);
         }
+        trace(YOUTH_SLAM_EV_SUBMIT_END, rc);
         // frames of this submission that ran in chained (micro-batch) launches
         g_batched.fetch_add(youth_icp_track_chained_frames(ctx) - chained0);
         // getSlamMapPoints reports the newest recorded frame: only the last
@@ -560,7 +635,7 @@ void worker_main(int device)
             if (i < sent)
                 pend.push_back(Pending{items[i].ts, i == m - 1 ? npts : -1, i == sent - 1, items[i]});
             else
-                queue_release(g_queue, items[i]);
+                queue_release(g_queue, items[i], N, pool_target(batch));
         }
         subs += sent > 0;
         if (batch == 1 && pend.size() == 2) finish_one(true);
@@ -667,6 +742,12 @@ void initSlamModule(const char* config_file, const char* vocabulary_file)
         g_queue->pinned = true;  // buffers the tracker copies to the device in place
     }
     youth_queue_clear(g_queue);
+    // page-locked buffers for the configured frame size (the YAML's, else
+    // 640x480) before the first frame: the producer never allocates them
+    {
+        const int pw = g_cfg_W > 0 ? g_cfg_W : 640, ph = g_cfg_H > 0 ? g_cfg_H : 480;
+        queue_prefill(g_queue, (size_t)pw * ph, pool_target(slam_batch()));
+    }
     g_traj.clear();
     g_traj_len.store(0, std::memory_order_release);
     g_last_points = 0;
@@ -815,6 +896,35 @@ int youth_slam_wait_idle(int timeout_ms)
         std::this_thread::sleep_for(std::chrono::milliseconds(1));
     }
     return 0;
+}
+
+int youth_slam_trace_enable(int capacity)
+{
+    if (capacity < 0) return YOUTH_EINVAL;
+    TraceEv* old = g_tr.exchange(nullptr, std::memory_order_acq_rel);
+    delete[] old;
+    g_tr_n.store(0, std::memory_order_relaxed);
+    g_tr_cap = 0;
+    if (capacity == 0) return YOUTH_OK;
+    TraceEv* b = new (std::nothrow) TraceEv[capacity];
+    if (!b) return YOUTH_ENOMEM;
+    g_tr_cap = capacity;
+    g_tr.store(b, std::memory_order_release);
+    return YOUTH_OK;
+}
+
+int youth_slam_trace_read(int n, double* t, int* kind, int* arg)
+{
+    TraceEv* b = g_tr.load(std::memory_order_acquire);
+    const int rec = g_tr_n.load(std::memory_order_acquire);
+    if (!b) return 0;
+    const int m = std::min(std::min(n, rec), g_tr_cap);
+    for (int i = 0; i < m; ++i) {
+        if (t) t[i] = b[i].t;
+        if (kind) kind[i] = b[i].kind;
+        if (arg) arg[i] = b[i].arg;
+    }
+    return rec;
 }
 
 void youth_slam_wait_stopped(void)

@@ -18,6 +18,11 @@
  * live latency median / p90 in microseconds, frames aligned in chained
  * launches, and a checksum of the last pass's world poses.
  *
+ * With YOUTH_SLAM_TRACE=<file> set, the module's event trace
+ * (youth_slam_trace_enable) covers the backlogged passes and is written to
+ * <file> as "t_seconds kind arg" lines (tools/slam_trace.py reads it beside a
+ * rocprofv3 kernel trace).
+ *
  * usage: slam_rate <n_frames> <passes> [width height]
  */
 #define _POSIX_C_SOURCE 200809L
@@ -66,6 +71,9 @@ int main(int argc, char** argv)
     youth_slam_wait_idle(20000);
     double rate[64], push_us[64], win[64][2];
     long long batched = 0;
+    const char* trace_path = getenv("YOUTH_SLAM_TRACE");
+    const int trace_cap = 1 << 20;
+    if (trace_path && youth_slam_trace_enable(trace_cap) != 0) return 7;
     for (int p = 0; p < passes; ++p) {
         resetSlam();
         youth_slam_wait_idle(20000);
@@ -86,6 +94,23 @@ int main(int argc, char** argv)
         rate[p] = n / (win[p][1] - t0);
         push_us[p] = in_push * 1e6 / n;
         batched += youth_slam_batched_frames() - b0;
+    }
+    if (trace_path) {
+        double* tt = (double*)malloc(trace_cap * sizeof(double));
+        int* tk = (int*)malloc(trace_cap * sizeof(int));
+        int* ta = (int*)malloc(trace_cap * sizeof(int));
+        if (!tt || !tk || !ta) return 3;
+        int ne = youth_slam_trace_read(trace_cap, tt, tk, ta);
+        if (ne > trace_cap) ne = trace_cap;
+        youth_slam_trace_enable(0);
+        FILE* f = fopen(trace_path, "w");
+        if (!f) return 8;
+        for (int p = 0; p < passes; ++p) fprintf(f, "# pass %d %.9f %.9f\n", p, win[p][0], win[p][1]);
+        for (int i = 0; i < ne; ++i) fprintf(f, "%.9f %d %d\n", tt[i], tk[i], ta[i]);
+        fclose(f);
+        free(tt);
+        free(tk);
+        free(ta);
     }
     const int got = youth_slam_get_trajectory(n, NULL, T);
     double sum = 0.0;

@@ -112,28 +112,38 @@ def gather_ragged(local: torch.Tensor, world: int, max_rows: int,
     return torch.cat([rows[r, : counts[r]] for r in range(world)])
 
 
-def rank_report(timings: dict, world: int) -> dict:
+def rank_report(timings: dict, world: int, values: dict | None = None) -> dict:
     """Every rank's timings (ms) in rank order plus what the process group
     itself reports, for an N > 1 bench line that proves its own shape
     (VERDICT r2 item 7): `rccl_world_size` / `backend` from the group, and
-    `per_rank_ms[name] = [rank 0, rank 1, ...]`.  Collective: every rank
-    calls it with the same keys.  No group (N = 1 without YOUTH_BENCH_DIST):
-    world size 1, this rank's values."""
+    `per_rank_ms[name] = [rank 0, rank 1, ...]`; `values` (non-time figures,
+    e.g. each rank's pose error against the CPU oracle) the same way under
+    `per_rank`.  Collective: every rank calls it with the same keys.  No group
+    (N = 1 without YOUTH_BENCH_DIST): world size 1, this rank's values."""
+    values = values or {}
     keys = sorted(timings)
-    vals = [float(timings[k]) for k in keys]
+    vkeys = sorted(values)
+    vals = [float(timings[k]) for k in keys] + [float(values[k]) for k in vkeys]
     if not dist.is_initialized():
-        return {"rccl_world_size": 1, "backend": None,
-                "per_rank_ms": {k: [v] for k, v in zip(keys, vals)}}
+        out = {"rccl_world_size": 1, "backend": None,
+               "per_rank_ms": {k: [float(timings[k])] for k in keys}}
+        if vkeys:
+            out["per_rank"] = {k: [float(values[k])] for k in vkeys}
+        return out
     backend = dist.get_backend()
     gw = dist.get_world_size()
     dev = "cuda" if backend == "nccl" else "cpu"
     t = torch.tensor(vals, dtype=torch.float64, device=dev)
-    out = torch.zeros(gw * len(keys), dtype=torch.float64, device=dev)
+    out = torch.zeros(gw * len(vals), dtype=torch.float64, device=dev)
     dist.all_gather_into_tensor(out, t)
-    rows = out.view(gw, len(keys)).cpu().numpy()
-    return {"rccl_world_size": int(gw), "backend": backend, "launch_world": int(world),
-            "per_rank_ms": {k: [float(rows[r, i]) for r in range(gw)]
-                            for i, k in enumerate(keys)}}
+    rows = out.view(gw, len(vals)).cpu().numpy()
+    rep = {"rccl_world_size": int(gw), "backend": backend, "launch_world": int(world),
+           "per_rank_ms": {k: [float(rows[r, i]) for r in range(gw)]
+                           for i, k in enumerate(keys)}}
+    if vkeys:
+        rep["per_rank"] = {k: [float(rows[r, len(keys) + i]) for r in range(gw)]
+                           for i, k in enumerate(vkeys)}
+    return rep
 
 
 def compose_trajectory(rel: np.ndarray) -> np.ndarray:

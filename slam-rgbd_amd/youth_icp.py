@@ -36,8 +36,8 @@ YOUTH_ENODEV = -4
 YOUTH_NEQ = 29
 SPEC_FMA = 0       # YOUTH_SPEC_FMA: opt-in, spec a7/a8 on fma chains
 SPEC_SURVEY = 1    # YOUTH_SPEC_SURVEY (default): SURVEY.md §8a a7/a8 as worded (no FMA, IEEE division)
-REDUCE_EXACT = 0   # YOUTH_REDUCE_EXACT: opt-in, every product exact in fp64
-REDUCE_LANE32 = 1  # YOUTH_REDUCE_LANE32 (default): SURVEY.md §8a a9, fp32 lanes -> fp64 finalize
+REDUCE_EXACT = 0   # YOUTH_REDUCE_EXACT (default): every product exact in fp64, launch-independent
+REDUCE_LANE32 = 1  # YOUTH_REDUCE_LANE32 (opt-in): fp32 lane sums -> fp64, launch-shape dependent
 LANES_STRIDED, LANES_COOP, LANES_COOP_TILE = 0, 1, 2   # youth_lanes.kind
 STATUS_DEGENERATE = 1
 STATUS_FEW_MATCHES = 2
@@ -165,6 +165,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "youth_slam_batched_frames": (ctypes.c_longlong, []),
         "youth_slam_queue_size": (c_int, []),
         "youth_slam_wait_stopped": (None, []),
+        "youth_slam_trace_enable": (c_int, [c_int]),
+        "youth_slam_trace_read": (c_int, [c_int, PD, POINTER(c_int), POINTER(c_int)]),
     }
     ab_build = bool(os.environ.get("YOUTH_ICP_LIB"))  # tools/ab_*.sh: older builds
     for name, (res, args) in sig.items():
@@ -272,6 +274,26 @@ def slam_batched_frames() -> int:
 def slam_queue_size() -> int:
     """Frames waiting in the SLAM module's ingest queue."""
     return load_library().youth_slam_queue_size()
+
+
+SLAM_EVENTS = {1: "push_begin", 2: "push_end", 3: "take", 4: "submit_begin", 5: "submit_end",
+               6: "collect_begin", 7: "collect_end", 8: "idle_begin", 9: "idle_end",
+               10: "pool", 11: "drop"}   # YOUTH_SLAM_EV_* (youth_icp.h)
+
+
+def slam_trace_enable(capacity: int) -> None:
+    """youth_slam_trace_enable: record the ingest path's events (0 = off)."""
+    _check(load_library().youth_slam_trace_enable(int(capacity)))
+
+
+def slam_trace_read(n: int = 1 << 20) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """(t seconds CLOCK_MONOTONIC, kind, arg) of the recorded events."""
+    t = np.zeros(n, np.float64)
+    k = np.zeros(n, np.int32)
+    a = np.zeros(n, np.int32)
+    m = min(n, load_library().youth_slam_trace_read(n, _p(t, c_double), _p(k, c_int),
+                                                     _p(a, c_int)))
+    return t[:m], k[:m], a[:m]
 
 
 def slam_trajectory() -> tuple[np.ndarray, np.ndarray]:

@@ -158,6 +158,34 @@ def test_queue_copies_frames():
     assert (d == np.arange(12).reshape(3, 4)).all() and ts == 1
 
 
+def test_ingest_trace_records_pushes_and_drops():
+    """youth_slam_trace_*: the producer side of the ingest path traces every
+    push (queue depth before, whether the buffer was pooled or new) and the
+    >10 -> 5 drops, lock-free, on any queue; reading returns the count
+    recorded; capacity 0 stops it."""
+    youth_icp.slam_trace_enable(64)
+    try:
+        q = youth_icp.FrameQueue(10, 5)
+        f = np.zeros((4, 6), np.int16)
+        for i in range(11):
+            q.push(f, i)
+        q.pop()
+        q.push(f, 11)                          # a buffer from the pool
+        t, k, a = youth_icp.slam_trace_read()
+        q.close()
+    finally:
+        youth_icp.slam_trace_enable(0)
+    names = [youth_icp.SLAM_EVENTS[int(v)] for v in k]
+    assert names.count("push_begin") == 12 and names.count("push_end") == 12
+    assert names.count("drop") == 1 and a[names.index("drop")] == 6
+    depth = [int(x) for x, n in zip(a, names) if n == "push_begin"]
+    assert depth[:11] == list(range(11)) and depth[11] == 4
+    kinds = [int(x) for x, n in zip(a, names) if n == "push_end"]
+    assert kinds[0] == 2 and kinds[-1] == 0      # new pageable, then pooled
+    assert (np.diff(t) >= 0).all()
+    assert youth_icp.slam_trace_read()[0].size == 0
+
+
 def test_parse_camera_yaml():
     K, W, H = youth_icp.parse_camera_yaml(os.path.join(GOLDEN, "astra_camera.yaml"))
     assert (K.fx, K.fy, K.cx, K.cy, K.depth_scale) == (np.float32(570.3), np.float32(570.3),

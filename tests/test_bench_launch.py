@@ -53,3 +53,18 @@ def test_mismatch_exits_before_torch():
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "2"], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "WORLD_SIZE 3" in r.stderr
+
+
+def test_rank_parity_sample_and_gate():
+    """each rank's sample (first two and last two pairs of
+    its shard) and the gate that makes rank 0 exit non-zero when any rank's
+    sampled poses are more than 1e-5 from the CPU oracle."""
+    b = _bench()
+    assert b.parity_sample(64) == [0, 1, 62, 63]
+    assert b.parity_sample(3) == [0, 1, 2] and b.parity_sample(1) == [0]
+    assert b.parity_sample(0) == []
+    ok = {"ranks": {"per_rank": {"pose_max_abs_err_vs_cpu": [2e-14, 9e-6]}}}
+    assert b.parity_gate(ok) and ok["parity_all_ranks_ok"] is True
+    bad = {"ranks": {"per_rank": {"pose_max_abs_err_vs_cpu": [2e-14, 1.1e-5]}}}
+    assert not b.parity_gate(bad) and bad["parity_all_ranks_ok"] is False
+    assert not b.parity_gate({"ranks": {}})                 # nothing checked is not a pass

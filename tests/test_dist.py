@@ -51,7 +51,9 @@ def _worker(rank, world, port, q):
         assert torch.equal(rows, rows_k)
         # bench.py's N > 1 self-report: the group's size and every rank's times
         rep = youth_dist.rank_report({"k_icp_ms": 1.0 + rank, "k_prep_ms": 0.1 * rank,
-                                      "gather_ms": 0.01}, world)
+                                      "gather_ms": 0.01}, world,
+                                     {"pose_max_abs_err_vs_cpu": 1e-9 * rank,
+                                      "pairs_checked": 4})
         q.put((rank, allp.numpy(), (f0, f1), rows.numpy(), rep))
     finally:
         dist.destroy_process_group()
@@ -74,6 +76,9 @@ def test_world2_gloo_shards_and_gather(world):
         assert rep["per_rank_ms"]["k_icp_ms"] == [1.0 + r for r in range(world)]
         assert np.allclose(rep["per_rank_ms"]["k_prep_ms"], [0.1 * r for r in range(world)])
         assert rep["per_rank_ms"]["gather_ms"] == [0.01] * world
+        # non-time figures (bench.py: each rank's pose check against the oracle)
+        assert rep["per_rank"]["pairs_checked"] == [4.0] * world
+        assert rep["per_rank"]["pose_max_abs_err_vs_cpu"] == [1e-9 * r for r in range(world)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -99,6 +104,8 @@ def test_world2_gloo_shards_and_gather(world):
 def test_rank_report_without_group():
     rep = youth_dist.rank_report({"k_icp_ms": 2.5}, 1)
     assert rep == {"rccl_world_size": 1, "backend": None, "per_rank_ms": {"k_icp_ms": [2.5]}}
+    rep = youth_dist.rank_report({"k_icp_ms": 2.5}, 1, {"pose_max_abs_err_vs_cpu": 3e-14})
+    assert rep["per_rank"] == {"pose_max_abs_err_vs_cpu": [3e-14]}
 
 
 def test_sequence_shard_edge_cases():

@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""Reads slam_rate's event trace (YOUTH_SLAM_TRACE=<file>, youth_slam_trace_*)
+and, optionally, the rocprofv3 kernel trace of the same run, and prints per
+backlogged pass: the rate, the micro-batches the worker formed (sizes), where
+the worker's time went (collect waits, submits, idle waits, the rest), the
+producer's push time, and the longest GPU-idle gap with the worker and
+producer events around it (which wait it sits in).
+
+usage: slam_trace.py TRACE [KERNEL_TRACE_CSV]
+"""
+import csv
+import sys
+
+KINDS = {1: "push_begin", 2: "push_end", 3: "take", 4: "submit_begin", 5: "submit_end",
+         6: "collect_begin", 7: "collect_end", 8: "idle_begin", 9: "idle_end", 10: "pool",
+         11: "drop"}
+
+
+def load(path):
+    passes, ev = [], []
+    with open(path) as f:
+        for ln in f:
+            if ln.startswith("# pass"):
+                _, _, p, t0, t1 = ln.split()
+                passes.append((float(t0), float(t1)))
+            elif ln.strip():
+                t, k, a = ln.split()
+                ev.append((float(t), int(k), int(a)))
+    return passes, ev
+
+
+def kernels(path):
+    out = []
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            out.append((int(row["Start_Timestamp"]) * 1e-9, int(row["End_Timestamp"]) * 1e-9,
+                        row["Kernel_Name"][:40]))
+    return sorted(out)
+
+
+def spans(ev, begin, end):
+    """(t_begin, t_end, arg_begin) of matched begin/end events."""
+    out, open_t = [], None
+    for t, k, a in ev:
+        if k == begin:
+            open_t = (t, a)
+        elif k == end and open_t is not None:
+            out.append((open_t[0], t, open_t[1]))
+            open_t = None
+    return out
+
+
+def main():
+    passes, ev = load(sys.argv[1])
+    ks = kernels(sys.argv[2]) if len(sys.argv) > 2 else None
+    for p, (t0, t1) in enumerate(passes):
+        e = [x for x in ev if t0 <= x[0] <= t1]
+        dur = t1 - t0
+        takes = [a for _, k, a in e if k == 3]
+        coll = spans(e, 6, 7)
+        subm = spans(e, 4, 5)
+        idle = spans(e, 8, 9)
+        push = spans(e, 1, 2)
+        pushes = [a for _, k, a in e if k == 2]
+        worker = sorted([(b, c, "collect") for b, c, _ in coll] + [(b, c, "submit") for b, c, _ in subm] +
+                        [(b, c, "idle") for b, c, _ in idle])
+        line = (f"pass {p}: {300 if not push else len(push)} frames {len(push) / dur:8.0f} frames/s "
+                f"{dur * 1e3:6.2f} ms | launches {len(subm)} sizes {sorted(takes)[:3]}..{sorted(takes)[-3:]} | "
+                f"worker collect {sum(c - b for b, c, _ in coll) * 1e3:5.2f} ms (max {max([c - b for b, c, _ in coll] or [0]) * 1e3:.2f}) "
+                f"submit {sum(c - b for b, c, _ in subm) * 1e3:5.2f} ms (max {max([c - b for b, c, _ in subm] or [0]) * 1e3:.2f}) "
+                f"idle {sum(c - b for b, c, _ in idle) * 1e3:5.2f} ms | producer push {sum(c - b for b, c, _ in push) * 1e3:5.2f} ms "
+                f"(max {max([c - b for b, c, _ in push] or [0]) * 1e3:.2f}), new buffers {sum(1 for a in pushes if a)}")
+        print(line)
+        # the longest stretch of the worker not inside a traced call, and the
+        # longest single traced call
+        gaps = [(worker[i + 1][0] - worker[i][1], worker[i][1], worker[i][2], worker[i + 1][2])
+                for i in range(len(worker) - 1)]
+        if gaps:
+            g = max(gaps)
+            print(f"    worker: longest untraced stretch {g[0] * 1e3:.3f} ms at +{(g[1] - t0) * 1e3:.2f} ms "
+                  f"(after {g[2]}, before {g[3]})")
+        if worker:
+            w = max(worker, key=lambda x: x[1] - x[0])
+            print(f"    worker: longest call {w[2]} {(w[1] - w[0]) * 1e3:.3f} ms at +{(w[0] - t0) * 1e3:.2f} ms")
+        if ks:
+            kk = [x for x in ks if x[1] >= t0 and x[0] <= t1]
+            if len(kk) > 1:
+                gi = max(range(len(kk) - 1), key=lambda i: kk[i + 1][0] - kk[i][1])
+                g0, g1 = kk[gi][1], kk[gi + 1][0]
+                print(f"    GPU: {len(kk)} kernels, longest idle gap {(g1 - g0) * 1e3:.3f} ms at "
+                      f"+{(g0 - t0) * 1e3:.2f} ms; events inside it:")
+                for t, k, a in e:
+                    if g0 - 2e-4 <= t <= g1 + 2e-4:
+                        print(f"      +{(t - t0) * 1e3:8.3f} ms {KINDS.get(k, k):14s} {a}")
+
+
+if __name__ == "__main__":
+    main()
