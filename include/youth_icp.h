@@ -264,7 +264,13 @@ void youth_icp_destroy(youth_icp_ctx* ctx);
  * GPU set YOUTH_ICP_COOP_LAUNCH=runtime (hipLaunchCooperativeKernel: the
  * runtime admits the grid or refuses it, and a refusal falls back to the
  * persistent kernel) or YOUTH_ICP_NO_COOP=1; a grid that is not co-resident
- * ends at the spin bound with YOUTH_STATUS_TIMEOUT, never a hang. */
+ * ends at the spin bound with YOUTH_STATUS_TIMEOUT, never a hang.  The
+ * first cooperative launch of the process from a second stream on a device
+ * waits once for that device to drain (hipDeviceSynchronize, without
+ * holding any lock: other threads' cooperative launches on the device wait
+ * for it, nothing else does); it fails (YOUTH_EHIP) if a stream on the
+ * device is being captured at that moment.  Later stream switches only
+ * order the launches through an event. */
 int youth_icp_align_pairs_device(youth_icp_ctx* ctx, const int16_t* d_src,
                                  const int16_t* d_dst, int n_pairs,
                                  const double* T_init, float* d_T_out,
@@ -531,6 +537,8 @@ void youth_slam_wait_stopped(void);
 #define YOUTH_SLAM_EV_IDLE_END      9  /* queue depth */
 #define YOUTH_SLAM_EV_POOL          10 /* worker: page-locked buffers allocated (+) / freed (-) */
 #define YOUTH_SLAM_EV_DROP          11 /* frames dropped by the >10 -> 5 policy */
+#define YOUTH_SLAM_EV_SUBMIT_STEP   12 /* inside a tracker submission: 1 slots ready, 2 waits
+                                          enqueued, 3 H2D copies enqueued, 4 H2D event, 5 launch */
 int youth_slam_trace_enable(int capacity);
 int youth_slam_trace_read(int n, double* t, int* kind, int* arg);
 

@@ -35,6 +35,7 @@
 #include <string.h>
 
 #include <chrono>
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -2405,6 +2406,25 @@ __global__ void k_finish(const double* __restrict__ T64, int n, float* __restric
     if (i == 0 && error && *error) status[t >> 4] |= YOUTH_STATUS_TIMEOUT;
 }
 
+// The tracker's H2D of m page-locked host frames by the GPU itself (A/B
+// against the SDMA copy engine, YOUTH_ICP_TRACK_COPY=kernel): 16-byte loads
+// straight from host memory, one 64-lane workgroup per slice, few VGPRs, so
+// its waves fit beside a resident cooperative grid.
+struct FramePtrs {
+    const int4* src[kCoopMaxChain];
+};
+__global__ __launch_bounds__(64) void k_pull_frames(FramePtrs fp, int4* __restrict__ dst,
+                                                    int vec_per_frame, int m)
+{
+    const int f = blockIdx.y;
+    if (f >= m) return;
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    const v4i* __restrict__ s = reinterpret_cast<const v4i*>(fp.src[f]);
+    v4i* __restrict__ d = reinterpret_cast<v4i*>(dst) + (size_t)f * vec_per_frame;
+    for (int i = blockIdx.x * 64 + threadIdx.x; i < vec_per_frame; i += gridDim.x * 64)
+        d[i] = __builtin_nontemporal_load(s + i);
+}
+
 // Per-pair status of one chunk of the host batch API, the launch's timeout
 // flag folded in (as youth_icp_get_poses does).
 __global__ void k_status_out(const int32_t* __restrict__ status, int n,
@@ -2489,6 +2509,8 @@ struct youth_icp_ctx {
     int coop_threads = 512;          // YOUTH_ICP_COOP_THREADS=256: one wave per SIMD
     int coop_max_pairs = kCoopMaxPairs;  // YOUTH_ICP_COOP_MAX_PAIRS (<= kCoopMaxPairs)
     int coop_launch = 0;             // YOUTH_ICP_COOP_LAUNCH: 0 serial (default), 1 runtime, 2 plain
+    bool trk_copy_compute = false;   // YOUTH_ICP_TRACK_COPY=compute: tracker H2D on the launch stream
+    bool trk_copy_kernel = false;    // YOUTH_ICP_TRACK_COPY=kernel: tracker H2D by k_pull_frames
     bool coop_refuse = false;        // YOUTH_ICP_TEST_REFUSE_COOP=1 (test hook)
     // occupancy of k_icp_coop<variant, fast, threads> [threads 256?][variant 2 + fast] at npx (LDS)
     int coop_bpc[2][2 * kVariants][kCoopMaxPx + 1] = {};
@@ -2848,10 +2870,12 @@ struct PrepJob {
 // YOUTH_ICP_COOP_LAUNCH=runtime restores hipLaunchCooperativeKernel.
 struct CoopOrder {
     std::mutex mu;
+    std::condition_variable cv;  // launches wait while the one-time drain runs
     hipStream_t last = nullptr;
     hipEvent_t done = nullptr;
     bool any = false;
-    bool multi = false;  // launches seen from more than one stream
+    bool multi = false;     // launches seen from more than one stream
+    bool draining = false;  // the first switch's device drain is in progress (mu released)
 };
 static CoopOrder g_coop_order[64];
 
@@ -2872,16 +2896,28 @@ static int coop_enqueue(youth_icp_ctx* c, hipStream_t s, void** args, int blocks
         return YOUTH_OK;
     }
     CoopOrder& o = g_coop_order[c->device];
-    std::lock_guard<std::mutex> lk(o.mu);
+    std::unique_lock<std::mutex> lk(o.mu);
+    o.cv.wait(lk, [&o] { return !o.draining; });
     if (o.any && o.last != s) {
         if (!o.done) HIP_TRY(hipEventCreateWithFlags(&o.done, hipEventDisableTiming));
         if (!o.multi) {
             // first switch: the previous stream may be a caller's stream that
             // has been destroyed since, so its handle is not used again
             // (ADVICE r3); the host waits once for the device to drain, which
-            // covers that stream's last coop grid.  From now on every launch
-            // records `done` on its own stream right after it
-            HIP_TRY(hipDeviceSynchronize());
+            // covers that stream's last coop grid.  The drain runs without
+            // holding mu: other threads' coop launches on this
+            // device wait on cv meanwhile (none may start before it ends),
+            // nothing else is blocked.  From now on every launch records
+            // `done` on its own stream right after it
+            o.draining = true;
+            lk.unlock();
+            const hipError_t e = hipDeviceSynchronize();
+            lk.lock();
+            o.draining = false;
+            o.cv.notify_all();
+            if (e != hipSuccess)
+                return set_error(YOUTH_EHIP, "coop launch: device drain on the first stream "
+                                             "switch: %s", hipGetErrorString(e));
             o.multi = true;
         } else {
             HIP_TRY(hipStreamWaitEvent(s, o.done, 0));
@@ -3393,6 +3429,9 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         c->coop_px_env = c->coop_px;
         const char* cl = getenv("YOUTH_ICP_COOP_LAUNCH");
         c->coop_launch = !cl ? 0 : strcmp(cl, "runtime") == 0 ? 1 : strcmp(cl, "plain") == 0 ? 2 : 0;
+        const char* tcp = getenv("YOUTH_ICP_TRACK_COPY");
+        c->trk_copy_compute = tcp && strcmp(tcp, "compute") == 0;
+        c->trk_copy_kernel = tcp && strcmp(tcp, "kernel") == 0;
         // test hook (tests/test_gpu_parity.py): every cooperative launch of
         // this context is refused as the runtime would, exercising the
         // persistent fallback of run_iterations
@@ -4038,6 +4077,10 @@ static bool trk_chain_fits(const youth_icp_ctx* c, int m)
 // reference).  One completion event for the launch, shared by its entries.
 // frames (nullable): the m frames are the caller's page-locked buffers,
 // copied H2D in place (no staging copy; youth_icp_track_submit_pinned).
+// the SLAM module's event trace (slam_api.cpp, youth_slam_trace_enable):
+// steps inside a submission, YOUTH_SLAM_EV_SUBMIT_STEP
+extern "C" void youth_slam_trace_hook(int kind, int arg);
+
 static int track_submit_frames(youth_icp_ctx* c, const int16_t* depth, int m,
                                const double* T_init, const int16_t* const* frames = nullptr)
 {
@@ -4059,20 +4102,54 @@ static int track_submit_frames(youth_icp_ctx* c, const int16_t* depth, int m,
         const int rc = track_entry_pinned(c, qi[i], !frames);  // before anything is enqueued
         if (rc) return rc;
     }
+    youth_slam_trace_hook(YOUTH_SLAM_EV_SUBMIT_STEP, 1);
     auto& ql = c->trk[qi[m - 1]];
     // the caller's buffers are free on return: copy into the entries' pinned
     // staging, then H2D after the last launch that read these depth slots
+    // the copies' stream: the transfer stream (overlaps the launch before),
+    // or with YOUTH_ICP_TRACK_COPY=compute the launch stream itself (A/B)
+    hipStream_t xs = c->trk_copy_compute ? s : c->xfer;
+    hipEvent_t waited[kCoopMaxChain];
+    int nw = 0;
     for (int i = 0; i < m; ++i) {
         if (!frames) memcpy(c->trk[qi[i]].pinned, depth + (size_t)i * N, N * sizeof(int16_t));
         const int last = c->trk_dslot_last[d0 + i];
-        if (last >= 0) HIP_TRY(hipStreamWaitEvent(c->xfer, c->trk[last].ev, 0));
+        if (last < 0 || xs == s) continue;
+        // the slots of one earlier launch share its event: wait once per event
+        hipEvent_t ev = c->trk[last].ev;
+        bool dup = false;
+        for (int k = 0; k < nw; ++k) dup |= waited[k] == ev;
+        if (!dup) {
+            HIP_TRY(hipStreamWaitEvent(xs, ev, 0));
+            waited[nw++] = ev;
+        }
     }
-    for (int i = 0; i < m; ++i)
-        HIP_TRY(hipMemcpyAsync(c->d_depth + (size_t)(d0 + i) * N,
-                               frames ? frames[i] : c->trk[qi[i]].pinned, N * sizeof(int16_t),
-                               hipMemcpyHostToDevice, c->xfer));
-    HIP_TRY(hipEventRecord(ql.h2d, c->xfer));
-    HIP_TRY(hipStreamWaitEvent(s, ql.h2d, 0));
+    youth_slam_trace_hook(YOUTH_SLAM_EV_SUBMIT_STEP, 2);
+    if (c->trk_copy_kernel && (N * sizeof(int16_t)) % 16 == 0) {
+        FramePtrs fp{};
+        bool aligned = true;
+        for (int i = 0; i < m; ++i) {
+            const int16_t* h = frames ? frames[i] : c->trk[qi[i]].pinned;
+            aligned &= ((uintptr_t)h & 15) == 0;
+            fp.src[i] = reinterpret_cast<const int4*>(h);
+        }
+        if (!aligned) return set_error(YOUTH_EINVAL, "track: frame buffers not 16-byte aligned");
+        const int vec = (int)(N * sizeof(int16_t) / 16);
+        hipLaunchKernelGGL(k_pull_frames, dim3(64, m), dim3(64), 0, xs, fp,
+                           reinterpret_cast<int4*>(c->d_depth + (size_t)d0 * N), vec, m);
+        HIP_TRY(hipGetLastError());
+    } else {
+        for (int i = 0; i < m; ++i)
+            HIP_TRY(hipMemcpyAsync(c->d_depth + (size_t)(d0 + i) * N,
+                                   frames ? frames[i] : c->trk[qi[i]].pinned, N * sizeof(int16_t),
+                                   hipMemcpyHostToDevice, xs));
+    }
+    youth_slam_trace_hook(YOUTH_SLAM_EV_SUBMIT_STEP, 3);
+    if (xs != s) {
+        HIP_TRY(hipEventRecord(ql.h2d, xs));
+        HIP_TRY(hipStreamWaitEvent(s, ql.h2d, 0));
+    }
+    youth_slam_trace_hook(YOUTH_SLAM_EV_SUBMIT_STEP, 4);
     const int16_t* dsrc = c->d_depth + (size_t)d0 * N;
     int rc = YOUTH_OK;
     bool kernel_result = false;  // k_icp_coop stored the result(s) to host memory
@@ -4106,6 +4183,7 @@ static int track_submit_frames(youth_icp_ctx* c, const int16_t* depth, int m,
         kernel_result = true;
         if (rc == YOUTH_OK) ++c->trk_chained;
     }
+    youth_slam_trace_hook(YOUTH_SLAM_EV_SUBMIT_STEP, 5);
     if (rc) {
         // nothing of these frames is kept; wait for what was enqueued so the
         // staging buffers and the slots are not in use by dropped frames

@@ -898,6 +898,9 @@ int youth_slam_wait_idle(int timeout_ms)
     return 0;
 }
 
+// recorded from inside the tracker (icp_kernels.hip: a submission's steps)
+void youth_slam_trace_hook(int kind, int arg) { trace(kind, arg); }
+
 int youth_slam_trace_enable(int capacity)
 {
     if (capacity < 0) return YOUTH_EINVAL;

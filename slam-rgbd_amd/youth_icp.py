@@ -278,7 +278,7 @@ def slam_queue_size() -> int:
 
 SLAM_EVENTS = {1: "push_begin", 2: "push_end", 3: "take", 4: "submit_begin", 5: "submit_end",
                6: "collect_begin", 7: "collect_end", 8: "idle_begin", 9: "idle_end",
-               10: "pool", 11: "drop"}   # YOUTH_SLAM_EV_* (youth_icp.h)
+               10: "pool", 11: "drop", 12: "submit_step"}   # YOUTH_SLAM_EV_* (youth_icp.h)
 
 
 def slam_trace_enable(capacity: int) -> None:

@@ -195,7 +195,7 @@ def test_off_centre_principal_point(monkeypatch):
         lanes = lanes_of(ctx)
         T32 = np.asarray(T64[0], np.float32)[:3]
         g_idx, g_neq = ctx.reduce(src[0], dst[0], T32)
-        rl = ctx.lanes()
+        rl = lanes_of(ctx)
     with oracle_like(lanes):
         To, sto, stats = oracle.align_batch(src, dst, K=Ko, iters=iters, n_threads=n,
                                             want_stats=True)

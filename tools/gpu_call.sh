@@ -10,6 +10,7 @@
 #   bench:ARGS   python bench.py ARGS (comma-separated, e.g. bench:--no-legs,--steps,50)
 #   profile      tools/profile.sh TAG (kernel trace + PMC passes)
 #   py:FILE      python FILE (a probe under tools/)
+#   sh:FILE      bash FILE (a multi-step probe under tools/, its own timeouts inside)
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out
@@ -39,6 +40,9 @@ for step in "$@"; do
     py)
       timeout -k 10 300 python -u $arg > $O/py_$(basename $arg .py)_$TAG.txt 2>&1 \
         || { tail -30 $O/py_$(basename $arg .py)_$TAG.txt; exit 6; } ;;
+    sh)
+      timeout -k 10 900 bash $arg > $O/sh_$(basename $arg .sh)_$TAG.txt 2>&1 \
+        || { tail -30 $O/sh_$(basename $arg .sh)_$TAG.txt; exit 7; } ;;
     *)
       echo "unknown step $step"; exit 9 ;;
   esac

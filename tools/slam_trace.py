@@ -13,7 +13,7 @@ import sys
 
 KINDS = {1: "push_begin", 2: "push_end", 3: "take", 4: "submit_begin", 5: "submit_end",
          6: "collect_begin", 7: "collect_end", 8: "idle_begin", 9: "idle_end", 10: "pool",
-         11: "drop"}
+         11: "drop", 12: "submit_step"}
 
 
 def load(path):
@@ -82,6 +82,19 @@ def main():
         if worker:
             w = max(worker, key=lambda x: x[1] - x[0])
             print(f"    worker: longest call {w[2]} {(w[1] - w[0]) * 1e3:.3f} ms at +{(w[0] - t0) * 1e3:.2f} ms")
+        # submissions over 1 ms: the time to each step inside them
+        cur = None
+        for t, k, a in e:
+            if k == 4:
+                cur = [t, a, []]
+            elif k == 12 and cur:
+                cur[2].append((a, t))
+            elif k == 5 and cur:
+                if t - cur[0] > 1e-3:
+                    steps = ", ".join(f"step {a} +{(ts - cur[0]) * 1e3:.3f}" for a, ts in cur[2])
+                    print(f"    slow submit of {cur[1]} frames at +{(cur[0] - t0) * 1e3:.2f} ms: "
+                          f"{(t - cur[0]) * 1e3:.3f} ms ({steps})")
+                cur = None
         if ks:
             kk = [x for x in ks if x[1] >= t0 and x[0] <= t1]
             if len(kk) > 1:
