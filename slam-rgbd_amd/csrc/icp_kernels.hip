@@ -2406,23 +2406,52 @@ __global__ void k_finish(const double* __restrict__ T64, int n, float* __restric
     if (i == 0 && error && *error) status[t >> 4] |= YOUTH_STATUS_TIMEOUT;
 }
 
-// The tracker's H2D of m page-locked host frames by the GPU itself (A/B
-// against the SDMA copy engine, YOUTH_ICP_TRACK_COPY=kernel): 16-byte loads
-// straight from host memory, one 64-lane workgroup per slice, few VGPRs, so
-// its waves fit beside a resident cooperative grid.
+// The tracker's H2D of m page-locked host frames, pulled by the GPU itself
+// (the default; YOUTH_ICP_TRACK_COPY=sdma uses hipMemcpyAsync on the copy
+// engine instead).  On the shared GPU hosts the SDMA path ran at 36-41 K
+// frames/s in quiet passes but stalled the submitting thread inside
+// hipMemcpyAsync for 8-18 ms about once in ten backlogged passes and fell to
+// ~9 K frames/s while the host was loaded; this kernel's passes stayed within
+// a few per cent of each other under the same conditions (DESIGN.md §6,
+// profiles/r05/).  Few 64-lane workgroups (a total of ~32 per launch), four
+// 16-byte loads in flight per lane, so its waves sit beside the resident
+// cooperative grid of the launch before it without slowing it much.
 struct FramePtrs {
-    const int4* src[kCoopMaxChain];
+    const int16_t* src[kCoopMaxChain];
 };
-__global__ __launch_bounds__(64) void k_pull_frames(FramePtrs fp, int4* __restrict__ dst,
-                                                    int vec_per_frame, int m)
+__global__ __launch_bounds__(64) void k_pull_frames(FramePtrs fp, int16_t* __restrict__ dst, int N,
+                                                    int m)
 {
     const int f = blockIdx.y;
     if (f >= m) return;
-    typedef int v4i __attribute__((ext_vector_type(4)));
-    const v4i* __restrict__ s = reinterpret_cast<const v4i*>(fp.src[f]);
-    v4i* __restrict__ d = reinterpret_cast<v4i*>(dst) + (size_t)f * vec_per_frame;
-    for (int i = blockIdx.x * 64 + threadIdx.x; i < vec_per_frame; i += gridDim.x * 64)
-        d[i] = __builtin_nontemporal_load(s + i);
+    const int16_t* __restrict__ s16 = fp.src[f];
+    int16_t* __restrict__ d16 = dst + (size_t)f * N;
+    const int stride = gridDim.x * 64;
+    const int t0 = blockIdx.x * 64 + threadIdx.x;
+    // 16-byte body when both ends are 16-byte aligned (page-locked buffers
+    // and W*H % 8 == 0 frames), else element by element
+    const bool vec = (((uintptr_t)s16 | (uintptr_t)d16) & 15) == 0;
+    int done = 0;
+    if (vec) {
+        typedef int v4i __attribute__((ext_vector_type(4)));
+        const v4i* __restrict__ s = reinterpret_cast<const v4i*>(s16);
+        v4i* __restrict__ d = reinterpret_cast<v4i*>(d16);
+        const int nv = N / 8;
+        int i = t0;
+        for (; i + 3 * stride < nv; i += 4 * stride) {
+            const v4i a = __builtin_nontemporal_load(s + i);
+            const v4i b = __builtin_nontemporal_load(s + i + stride);
+            const v4i c = __builtin_nontemporal_load(s + i + 2 * stride);
+            const v4i e = __builtin_nontemporal_load(s + i + 3 * stride);
+            d[i] = a;
+            d[i + stride] = b;
+            d[i + 2 * stride] = c;
+            d[i + 3 * stride] = e;
+        }
+        for (; i < nv; i += stride) d[i] = __builtin_nontemporal_load(s + i);
+        done = nv * 8;
+    }
+    for (int i = done + t0; i < N; i += stride) d16[i] = s16[i];
 }
 
 // Per-pair status of one chunk of the host batch API, the launch's timeout
@@ -2510,7 +2539,8 @@ struct youth_icp_ctx {
     int coop_max_pairs = kCoopMaxPairs;  // YOUTH_ICP_COOP_MAX_PAIRS (<= kCoopMaxPairs)
     int coop_launch = 0;             // YOUTH_ICP_COOP_LAUNCH: 0 serial (default), 1 runtime, 2 plain
     bool trk_copy_compute = false;   // YOUTH_ICP_TRACK_COPY=compute: tracker H2D on the launch stream
-    bool trk_copy_kernel = false;    // YOUTH_ICP_TRACK_COPY=kernel: tracker H2D by k_pull_frames
+    bool trk_copy_sdma = false;      // YOUTH_ICP_TRACK_COPY=sdma: hipMemcpyAsync, not k_pull_frames
+    int trk_pull_wg = 0;             // YOUTH_ICP_PULL_WG: k_pull_frames workgroups per frame (0: auto)
     bool coop_refuse = false;        // YOUTH_ICP_TEST_REFUSE_COOP=1 (test hook)
     // occupancy of k_icp_coop<variant, fast, threads> [threads 256?][variant 2 + fast] at npx (LDS)
     int coop_bpc[2][2 * kVariants][kCoopMaxPx + 1] = {};
@@ -3431,7 +3461,9 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         c->coop_launch = !cl ? 0 : strcmp(cl, "runtime") == 0 ? 1 : strcmp(cl, "plain") == 0 ? 2 : 0;
         const char* tcp = getenv("YOUTH_ICP_TRACK_COPY");
         c->trk_copy_compute = tcp && strcmp(tcp, "compute") == 0;
-        c->trk_copy_kernel = tcp && strcmp(tcp, "kernel") == 0;
+        c->trk_copy_sdma = tcp && (strcmp(tcp, "sdma") == 0 || c->trk_copy_compute);
+        const char* pwg = getenv("YOUTH_ICP_PULL_WG");
+        c->trk_pull_wg = pwg && atoi(pwg) > 0 ? std::min(atoi(pwg), 1024) : 0;
         // test hook (tests/test_gpu_parity.py): every cooperative launch of
         // this context is refused as the runtime would, exercising the
         // persistent fallback of run_iterations
@@ -4125,18 +4157,14 @@ static int track_submit_frames(youth_icp_ctx* c, const int16_t* depth, int m,
         }
     }
     youth_slam_trace_hook(YOUTH_SLAM_EV_SUBMIT_STEP, 2);
-    if (c->trk_copy_kernel && (N * sizeof(int16_t)) % 16 == 0) {
+    if (!c->trk_copy_sdma) {
         FramePtrs fp{};
-        bool aligned = true;
-        for (int i = 0; i < m; ++i) {
-            const int16_t* h = frames ? frames[i] : c->trk[qi[i]].pinned;
-            aligned &= ((uintptr_t)h & 15) == 0;
-            fp.src[i] = reinterpret_cast<const int4*>(h);
-        }
-        if (!aligned) return set_error(YOUTH_EINVAL, "track: frame buffers not 16-byte aligned");
-        const int vec = (int)(N * sizeof(int16_t) / 16);
-        hipLaunchKernelGGL(k_pull_frames, dim3(64, m), dim3(64), 0, xs, fp,
-                           reinterpret_cast<int4*>(c->d_depth + (size_t)d0 * N), vec, m);
+        for (int i = 0; i < m; ++i) fp.src[i] = frames ? frames[i] : c->trk[qi[i]].pinned;
+        // ~32 workgroups per launch: 4 per frame in a micro-batch of 8, 32 for
+        // a single frame (its latency)
+        const int wg = c->trk_pull_wg > 0 ? c->trk_pull_wg : std::max(4, 32 / m);
+        hipLaunchKernelGGL(k_pull_frames, dim3(wg, m), dim3(64), 0, xs, fp, c->d_depth + (size_t)d0 * N,
+                           (int)N, m);
         HIP_TRY(hipGetLastError());
     } else {
         for (int i = 0; i < m; ++i)

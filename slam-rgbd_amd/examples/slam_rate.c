@@ -66,9 +66,22 @@ int main(int argc, char** argv)
         fprintf(stderr, "slam_rate: module did not start (no HIP device?)\n");
         return 4;
     }
-    /* warm: the worker's context, its plan and the page-locked queue pool */
+    /* warm: the worker's context, its plan and the page-locked queue pool;
+     * SLAM_RATE_WARM_PASSES=k adds k untimed backlogged passes */
     for (int k = 0; k < n && k < 24; ++k) processSlamFrame(frames + (size_t)k * N, NULL, W, H, k);
     youth_slam_wait_idle(20000);
+    const char* wp = getenv("SLAM_RATE_WARM_PASSES");
+    for (int p = 0; wp && p < atoi(wp); ++p) {
+        resetSlam();
+        youth_slam_wait_idle(20000);
+        for (int k = 0; k < n; ++k) {
+            while (youth_slam_queue_size() >= 10) {
+            }
+            processSlamFrame(frames + (size_t)k * N, NULL, W, H, (uint32_t)k);
+        }
+        while (youth_slam_trajectory_length() < n) {
+        }
+    }
     double rate[64], push_us[64], win[64][2];
     long long batched = 0;
     const char* trace_path = getenv("YOUTH_SLAM_TRACE");

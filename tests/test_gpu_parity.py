@@ -1301,3 +1301,48 @@ def test_track_micro_batches_up_to_four(batch):
         Tb, stb = ctx.track_host_sequence(frames)
         assert np.array_equal(Tb, np.stack([w[0] for w in want[1:]]))
         assert np.array_equal(stb, np.array([w[1] for w in want[1:]], np.int32))
+
+
+@pytest.mark.parametrize("W,H", [(640, 480), (97, 53)])
+def test_track_frame_copy_paths_bit_identical(monkeypatch, W, H):
+    """The tracker's H2D of host frames: k_pull_frames (the default: the GPU
+    pulls the page-locked frames itself, 16-byte body when both ends are
+    aligned, element tail; 97x53 frames are 10,282 bytes, so every other
+    device slot is misaligned and takes the element path) against the SDMA
+    copy engine (YOUTH_ICP_TRACK_COPY=sdma): the same poses bit for bit, one
+    frame per launch and in micro-batches of 4, through track_host_sequence
+    (staged copies) and track_submit_pinned (the caller's page-locked
+    buffers)."""
+    frames, _ = youth_synth.sequence(17, 9, W, H)
+    K = youth_icp.default_intrinsics(W, H)
+    res = {}
+    for path in ("sdma", "pull"):
+        if path == "sdma":
+            monkeypatch.setenv("YOUTH_ICP_TRACK_COPY", "sdma")
+        else:
+            monkeypatch.delenv("YOUTH_ICP_TRACK_COPY", raising=False)
+        out = []
+        for batch in (1, 4):
+            with youth_icp.IcpContext(W, H, 8, K=K) as ctx:
+                if batch > 1:
+                    ctx.track_set_batch(batch)
+                out.append(ctx.track_host_sequence(frames)[0])
+                ctx.track_reset()
+                bufs = [youth_icp.PinnedFrame(H, W) for _ in frames]
+                for b, f in zip(bufs, frames):
+                    b.array[:] = f
+                got = []
+                for i in range(0, len(bufs), batch):
+                    ctx.track_submit_pinned(bufs[i:i + batch])
+                    while ctx.track_pending():
+                        T, _, has = ctx.track_collect()
+                        if has:
+                            got.append(T)
+                out.append(np.stack(got))
+                for b in bufs:
+                    b.close()
+        res[path] = out
+    for a, b in zip(res["sdma"], res["pull"]):
+        assert np.array_equal(a, b)
+    T64, _, _, _ = oracle.align(frames[1], frames[0])
+    assert _pose_err(res["pull"][0][0], T64) <= POSE_TOL

@@ -1,17 +1,19 @@
 #!/bin/bash
 # The drop-in path's backlogged passes (examples/slam_rate, plain-C producer)
-# under a rocprofv3 kernel trace with the module's event trace on, then
-# tools/slam_trace.py per pass.  Output: gpurun_out/slamtrace/.
+# under a rocprofv3 kernel + copy trace with the module's event trace on, per
+# tracker copy path (SDMA, or k_pull_frames: YOUTH_ICP_TRACK_COPY=kernel);
+# tools/slam_trace.py per pass, and the overlap of the copies with k_icp_coop.
 set -eo pipefail
 export TMPDIR=/tmp
-O=gpurun_out/slamtrace
+O=gpurun_out/slamtrace5
 mkdir -p $O
-YOUTH_SLAM_TRACE=$O/events.txt timeout -k 10 120 rocprofv3 --kernel-trace --memory-copy-trace \
-    --output-format csv -d $O/kt -o kt -- slam-rgbd_amd/slam_rate 300 9 > $O/slam_rate.json 2> $O/slam_rate.err
-KT=$(find $O/kt -name '*kernel_trace.csv' -print -quit)
-python3 tools/slam_trace.py $O/events.txt $KT > $O/summary.txt
-cat $O/summary.txt
-# the same without the profiler (its overhead can shift the timing)
-YOUTH_SLAM_TRACE=$O/events_noprof.txt timeout -k 10 120 slam-rgbd_amd/slam_rate 300 9 > $O/slam_rate_noprof.json
-python3 tools/slam_trace.py $O/events_noprof.txt > $O/summary_noprof.txt
-cat $O/summary_noprof.txt
+for cfg in "kernel YOUTH_ICP_TRACK_COPY=kernel" "sdma"; do
+  set -- $cfg
+  label=$1; shift
+  env "$@" YOUTH_SLAM_TRACE=$O/events_$label.txt timeout -k 10 120 rocprofv3 --kernel-trace --memory-copy-trace \
+      --output-format csv -d $O/kt_$label -o kt -- slam-rgbd_amd/slam_rate 300 6 > $O/slam_rate_$label.json 2> $O/slam_rate_$label.err
+  KT=$(find $O/kt_$label -name '*kernel_trace.csv' -print -quit)
+  python3 tools/slam_trace.py $O/events_$label.txt $KT > $O/summary_$label.txt
+  echo "== $label"; grep "^pass\|slow submit" $O/summary_$label.txt
+  python3 tools/copy_overlap.py $O/kt_$label
+done
