@@ -36,6 +36,7 @@
 
 #include <chrono>
 #include <condition_variable>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -4109,9 +4110,32 @@ static bool trk_chain_fits(const youth_icp_ctx* c, int m)
 // reference).  One completion event for the launch, shared by its entries.
 // frames (nullable): the m frames are the caller's page-locked buffers,
 // copied H2D in place (no staging copy; youth_icp_track_submit_pinned).
+// Page-locked buffers handed out by youth_icp_host_alloc, by base address:
+// k_pull_frames reads a caller's frame in place only when it lies inside one
+// of them (youth_icp_track_submit_pinned); any other pointer goes through
+// hipMemcpyAsync, so a pageable buffer passed by mistake is copied by the
+// runtime instead of faulting the GPU.
+static std::mutex g_host_mu;
+static std::map<uintptr_t, size_t> g_host_bufs;  // base -> bytes
+
+static bool host_alloc_covers(const int16_t* p, size_t values)
+{
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    auto it = g_host_bufs.upper_bound(a);
+    if (it == g_host_bufs.begin()) return false;
+    --it;
+    return a >= it->first && a + values * sizeof(int16_t) <= it->first + it->second;
+}
+
 // the SLAM module's event trace (slam_api.cpp, youth_slam_trace_enable):
-// steps inside a submission, YOUTH_SLAM_EV_SUBMIT_STEP
-extern "C" void youth_slam_trace_hook(int kind, int arg);
+// steps inside a submission, YOUTH_SLAM_EV_SUBMIT_STEP.  Weak: tools that
+// compile this file without slam_api.cpp (tools/coopbench ...) record nothing.
+extern "C" __attribute__((weak)) void youth_slam_trace_hook(int kind, int arg);
+static inline void trace_step(int step)
+{
+    if (youth_slam_trace_hook) youth_slam_trace_hook(YOUTH_SLAM_EV_SUBMIT_STEP, step);
+}
 
 static int track_submit_frames(youth_icp_ctx* c, const int16_t* depth, int m,
                                const double* T_init, const int16_t* const* frames = nullptr)
@@ -4134,7 +4158,7 @@ static int track_submit_frames(youth_icp_ctx* c, const int16_t* depth, int m,
         const int rc = track_entry_pinned(c, qi[i], !frames);  // before anything is enqueued
         if (rc) return rc;
     }
-    youth_slam_trace_hook(YOUTH_SLAM_EV_SUBMIT_STEP, 1);
+    trace_step(1);
     auto& ql = c->trk[qi[m - 1]];
     // the caller's buffers are free on return: copy into the entries' pinned
     // staging, then H2D after the last launch that read these depth slots
@@ -4156,8 +4180,12 @@ static int track_submit_frames(youth_icp_ctx* c, const int16_t* depth, int m,
             waited[nw++] = ev;
         }
     }
-    youth_slam_trace_hook(YOUTH_SLAM_EV_SUBMIT_STEP, 2);
-    if (!c->trk_copy_sdma) {
+    trace_step(2);
+    // the caller's frames are pulled in place only when youth_icp_host_alloc
+    // made them (the staging buffers always are page-locked)
+    bool pull = !c->trk_copy_sdma;
+    for (int i = 0; pull && frames && i < m; ++i) pull = host_alloc_covers(frames[i], N);
+    if (pull) {
         FramePtrs fp{};
         for (int i = 0; i < m; ++i) fp.src[i] = frames ? frames[i] : c->trk[qi[i]].pinned;
         // ~32 workgroups per launch: 4 per frame in a micro-batch of 8, 32 for
@@ -4172,12 +4200,12 @@ static int track_submit_frames(youth_icp_ctx* c, const int16_t* depth, int m,
                                    frames ? frames[i] : c->trk[qi[i]].pinned, N * sizeof(int16_t),
                                    hipMemcpyHostToDevice, xs));
     }
-    youth_slam_trace_hook(YOUTH_SLAM_EV_SUBMIT_STEP, 3);
+    trace_step(3);
     if (xs != s) {
         HIP_TRY(hipEventRecord(ql.h2d, xs));
         HIP_TRY(hipStreamWaitEvent(s, ql.h2d, 0));
     }
-    youth_slam_trace_hook(YOUTH_SLAM_EV_SUBMIT_STEP, 4);
+    trace_step(4);
     const int16_t* dsrc = c->d_depth + (size_t)d0 * N;
     int rc = YOUTH_OK;
     bool kernel_result = false;  // k_icp_coop stored the result(s) to host memory
@@ -4211,7 +4239,7 @@ static int track_submit_frames(youth_icp_ctx* c, const int16_t* depth, int m,
         kernel_result = true;
         if (rc == YOUTH_OK) ++c->trk_chained;
     }
-    youth_slam_trace_hook(YOUTH_SLAM_EV_SUBMIT_STEP, 5);
+    trace_step(5);
     if (rc) {
         // nothing of these frames is kept; wait for what was enqueued so the
         // staging buffers and the slots are not in use by dropped frames
@@ -4308,12 +4336,19 @@ int16_t* youth_icp_host_alloc(size_t values)
         (void)hipGetLastError();
         return nullptr;
     }
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    g_host_bufs[(uintptr_t)p] = values * sizeof(int16_t);
     return p;
 }
 
 void youth_icp_host_free(int16_t* p)
 {
-    if (p) (void)hipHostFree(p);
+    if (!p) return;
+    {
+        std::lock_guard<std::mutex> lk(g_host_mu);
+        g_host_bufs.erase((uintptr_t)p);
+    }
+    (void)hipHostFree(p);
 }
 
 // A collect waits for its frame by polling the event for up to 2 ms before

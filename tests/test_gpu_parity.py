@@ -1346,3 +1346,40 @@ def test_track_frame_copy_paths_bit_identical(monkeypatch, W, H):
         assert np.array_equal(a, b)
     T64, _, _, _ = oracle.align(frames[1], frames[0])
     assert _pose_err(res["pull"][0][0], T64) <= POSE_TOL
+
+
+def test_track_submit_pinned_pageable_buffers_fall_back():
+    """youth_icp_track_submit_pinned with buffers youth_icp_host_alloc did not
+    make (pageable numpy arrays, a contract violation): the GPU must not read
+    them in place (that would fault); the submission takes hipMemcpyAsync and
+    the poses equal those from page-locked buffers bit for bit."""
+    import ctypes
+
+    class NumpyFrame:
+        def __init__(self, a):
+            self.array = np.ascontiguousarray(a)
+            self.ptr = self.array.ctypes.data_as(ctypes.POINTER(ctypes.c_int16))
+
+    frames, _ = youth_synth.sequence(19, 5)
+    out = []
+    for make in (lambda f: NumpyFrame(f), None):
+        with youth_icp.IcpContext(640, 480, 8) as ctx:
+            ctx.track_set_batch(4)
+            if make is None:
+                bufs = [youth_icp.PinnedFrame(480, 640) for _ in frames]
+                for b, f in zip(bufs, frames):
+                    b.array[:] = f
+            else:
+                bufs = [make(f) for f in frames]
+            got = []
+            ctx.track_submit_pinned(bufs[:1])
+            ctx.track_submit_pinned(bufs[1:])
+            while ctx.track_pending():
+                T, _, has = ctx.track_collect()
+                if has:
+                    got.append(T)
+            out.append(np.stack(got))
+            if make is None:
+                for b in bufs:
+                    b.close()
+    assert np.array_equal(out[0], out[1])
