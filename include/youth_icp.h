@@ -525,9 +525,10 @@ void youth_slam_wait_stopped(void);
  * youth_slam_trace_enable(0) stops recording and frees the buffer.  Enable
  * or disable only while no frame is being pushed.  youth_slam_trace_read
  * copies up to n events (t[n] seconds, kind[n], arg[n]) and returns how many
- * were recorded (may exceed n).  Kinds and their arg: */
+ * were recorded (at most the capacity; may exceed n).  Kinds and their arg: */
 #define YOUTH_SLAM_EV_PUSH_BEGIN    1  /* queue depth before the push */
-#define YOUTH_SLAM_EV_PUSH_END      2  /* buffer: 0 pooled, 1 new page-locked, 2 new pageable */
+#define YOUTH_SLAM_EV_PUSH_END      2  /* buffer: 0 pooled, 2 new pageable (1 unused: the
+                                          producer never allocates page-locked memory) */
 #define YOUTH_SLAM_EV_TAKE          3  /* frames in the micro-batch being formed */
 #define YOUTH_SLAM_EV_SUBMIT_BEGIN  4  /* frames submitted */
 #define YOUTH_SLAM_EV_SUBMIT_END    5  /* return code */

@@ -56,7 +56,8 @@ double mono_s()
 void trace(int kind, int arg)
 {
     TraceEv* b = g_tr.load(std::memory_order_acquire);
-    if (!b) return;
+    // a full buffer stops counting (the count never wraps)
+    if (!b || g_tr_n.load(std::memory_order_relaxed) >= g_tr_cap) return;
     const int i = g_tr_n.fetch_add(1, std::memory_order_relaxed);
     if (i < g_tr_cap) b[i] = TraceEv{mono_s(), kind, arg};
 }
@@ -120,9 +121,8 @@ void buf_free(youth_frame_queue* q, youth_frame_queue::Item& it)
 }
 
 // A buffer of >= n values for the producer: a pooled one, else (no pooled
-// buffer fits, or the queue is not page-locked) a new pageable one.  *kind:
-// 0 pooled, 1 new page-locked, 2 new pageable.  No page-locked allocation on
-// this path when q->pinned (the worker does those).
+// buffer fits) a new pageable one.  *kind: 0 pooled, 2 new pageable (this
+// path never allocates page-locked memory: the worker and init do).
 bool buf_get(youth_frame_queue* q, size_t n, youth_frame_queue::Item& it, int* kind)
 {
     {
