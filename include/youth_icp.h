@@ -441,8 +441,10 @@ void youth_icp_host_free(int16_t* p);
 /* Frames per submission youth_icp_track_host_sequence uses (1, default: one
  * launch per frame; up to YOUTH_TRACK_MAX_BATCH: micro-batches).  Batch mode
  * (> 1) plans the context's cooperative launches with the fewest source
- * pixels per lane that let that many pairs share one grid (640x480: 5, 8,
- * 10 and 19 px per lane for 2, 3, 4 and 8 frames), so results stay bit-identical between
+ * pixels per lane that let that many pairs share one grid on the chip less
+ * 32 CUs (kept free for the next micro-batch's frame pull, k_pull_frames;
+ * YOUTH_ICP_PULL_RESERVE_CU overrides; 640x480: 6, 9, 11 and 22 px per lane
+ * for 2, 3, 4 and 8 frames), so results stay bit-identical between
  * batched and per-frame submission on that context (and within 1e-13 of the
  * oracle, like the default plan).
  * Returns the previous value or YOUTH_EINVAL. */

@@ -2542,6 +2542,8 @@ struct youth_icp_ctx {
     bool trk_copy_compute = false;   // YOUTH_ICP_TRACK_COPY=compute: tracker H2D on the launch stream
     bool trk_copy_sdma = false;      // YOUTH_ICP_TRACK_COPY=sdma: hipMemcpyAsync, not k_pull_frames
     int trk_pull_wg = 0;             // YOUTH_ICP_PULL_WG: k_pull_frames workgroups per frame (0: auto)
+    int trk_pull_lds = 48 << 10;     // YOUTH_ICP_PULL_LDS: LDS bytes a k_pull_frames workgroup reserves
+    int trk_pull_reserve = 32;       // YOUTH_ICP_PULL_RESERVE_CU: CUs a micro-batch plan leaves free
     bool coop_refuse = false;        // YOUTH_ICP_TEST_REFUSE_COOP=1 (test hook)
     // occupancy of k_icp_coop<variant, fast, threads> [threads 256?][variant 2 + fast] at npx (LDS)
     int coop_bpc[2][2 * kVariants][kCoopMaxPx + 1] = {};
@@ -3465,6 +3467,10 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         c->trk_copy_sdma = tcp && (strcmp(tcp, "sdma") == 0 || c->trk_copy_compute);
         const char* pwg = getenv("YOUTH_ICP_PULL_WG");
         c->trk_pull_wg = pwg && atoi(pwg) > 0 ? std::min(atoi(pwg), 1024) : 0;
+        const char* plds = getenv("YOUTH_ICP_PULL_LDS");
+        if (plds && atoi(plds) >= 0) c->trk_pull_lds = std::min(atoi(plds), 64 << 10);
+        const char* pres = getenv("YOUTH_ICP_PULL_RESERVE_CU");
+        if (pres && atoi(pres) >= 0) c->trk_pull_reserve = atoi(pres);
         // test hook (tests/test_gpu_parity.py): every cooperative launch of
         // this context is refused as the runtime would, exercising the
         // persistent fallback of run_iterations
@@ -4188,11 +4194,16 @@ static int track_submit_frames(youth_icp_ctx* c, const int16_t* depth, int m,
     if (pull) {
         FramePtrs fp{};
         for (int i = 0; i < m; ++i) fp.src[i] = frames ? frames[i] : c->trk[qi[i]].pinned;
-        // ~32 workgroups per launch: 4 per frame in a micro-batch of 8, 32 for
-        // a single frame (its latency)
-        const int wg = c->trk_pull_wg > 0 ? c->trk_pull_wg : std::max(4, 32 / m);
-        hipLaunchKernelGGL(k_pull_frames, dim3(wg, m), dim3(64), 0, xs, fp, c->d_depth + (size_t)d0 * N,
-                           (int)N, m);
+        // ~16 workgroups per launch: 2 per frame in a micro-batch of 8 (one
+        // per free CU, profiles/r05/slam_pull_reserve_r5s.txt), 16 for a
+        // single frame (its latency)
+        const int wg = c->trk_pull_wg > 0 ? c->trk_pull_wg : std::max(2, 16 / m);
+        // its LDS reservation (unused) keeps a workgroup off the CUs where a
+        // micro-batch grid's workgroup sits (~143 KB of 160 at 640x480), so
+        // the pull runs on the CUs the plan left free instead of slowing the
+        // grid's barriers (youth_icp_track_set_batch)
+        hipLaunchKernelGGL(k_pull_frames, dim3(wg, m), dim3(64), (unsigned)c->trk_pull_lds, xs, fp,
+                           c->d_depth + (size_t)d0 * N, (int)N, m);
         HIP_TRY(hipGetLastError());
     } else {
         for (int i = 0; i < m; ++i)
@@ -4478,10 +4489,14 @@ int youth_icp_track_set_batch(youth_icp_ctx* c, int frames)
     c->coop_px = c->coop_px_env;
     if (frames > 1) {
         const int v = variant(c) * 2 + (c->fast ? 1 : 0);
+        // the plan leaves trk_pull_reserve CUs free for the next micro-batch's
+        // k_pull_frames (the co-residency limit itself stays the whole chip);
+        // the same plan on either copy path, so their poses are bit-identical
+        const int free_cu = std::min(c->trk_pull_reserve, c->n_cu / 2);
         for (int npx = 1; npx <= kCoopMaxPx; ++npx) {
             const long long G = (c->N + (long long)npx * c->coop_threads - 1) /
                                 ((long long)npx * c->coop_threads);
-            if (frames * G <= (long long)c->n_cu * c->coop_bpc[c->coop_threads == 256][v][npx]) {
+            if (frames * G <= (long long)(c->n_cu - free_cu) * c->coop_bpc[c->coop_threads == 256][v][npx]) {
                 c->coop_px = npx;
                 break;
             }

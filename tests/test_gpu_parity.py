@@ -1262,8 +1262,9 @@ def test_track_micro_batches_ragged_sizes(W, H, spec):
 @pytest.mark.parametrize("batch", [3, 4])
 def test_track_micro_batches_up_to_four(batch):
     """Micro-batches of up to TRACK_MAX_BATCH frames (youth_icp_track_set_batch(
-    batch): the plan whose `batch` grids fit the chip at once, 8 / 10 px per
-    lane at 640x480): chains of 4, 3 and 2 frames, a submission longer than
+    batch): the plan whose `batch` grids fit the chip at once less the 32 CUs
+    kept free for the next micro-batch's k_pull_frames, 9 / 11 px per lane at
+    640x480): chains of 4, 3 and 2 frames, a submission longer than
     the plan holds split into the longest chains that fit, and the library
     loop with two submissions in flight, every frame bit-identical to
     track_frame in the same plan and within 1e-5 of the oracle."""
@@ -1272,7 +1273,7 @@ def test_track_micro_batches_up_to_four(batch):
         ref.track_set_batch(batch)
         want = [ref.track_frame(f) for f in frames]
         plan = ref.get_plan()
-    assert plan["px_per_lane"] == {3: 8, 4: 10}[batch]
+    assert plan["px_per_lane"] == {3: 9, 4: 11}[batch]
     for k in range(1, len(frames)):
         T64, _, sto, _ = oracle.align(frames[k], frames[k - 1])
         assert want[k][1] == sto and _pose_err(want[k][0], T64) <= POSE_TOL
