@@ -605,6 +605,45 @@ def test_slam_worker_micro_batches(monkeypatch, batch):
         assert _pose_err(T[k], acc_o) <= POSE_TOL
 
 
+def test_slam_ingest_trace_accounts_for_every_frame():
+    """youth_slam_trace_*: over a backlog of 30 frames pushed as a producer
+    would (waiting while 10 are queued), the trace holds one push begin/end
+    per frame with no pool miss (initSlamModule pre-filled the page-locked
+    pool), micro-batches whose sizes add up to the frames taken, every
+    submission with its five steps in order and a zero return code, one
+    collect per frame, and timestamps inside the run."""
+    F = 30
+    frames, _ = youth_synth.sequence(3, F)
+    lib = youth_icp.load_library()
+    youth_icp.initSlamModule(None)
+    try:
+        youth_icp.slam_trace_enable(1 << 16)
+        for k in range(F):
+            while lib.youth_slam_queue_size() >= 10:
+                pass
+            assert youth_icp.processSlamFrame(frames[k], None, 640, 480, k) == 1
+        assert youth_icp.slam_wait_idle(20000) == 1
+        t, kind, arg = youth_icp.slam_trace_read()
+        assert youth_icp.slam_trajectory()[0].size == F
+    finally:
+        youth_icp.slam_trace_enable(0)
+        youth_icp.stopSlamModule()
+    names = [youth_icp.SLAM_EVENTS[int(v)] for v in kind]
+    ev = list(zip(names, (int(a) for a in arg)))
+    assert names.count("push_begin") == F and names.count("push_end") == F
+    assert all(a == 0 for n, a in ev if n == "push_end")          # every buffer pooled
+    assert "drop" not in names
+    assert sum(a for n, a in ev if n == "take") == F
+    assert names.count("collect_end") == F
+    subs = [i for i, n in enumerate(names) if n == "submit_begin"]
+    assert len(subs) == names.count("submit_end") == names.count("take")
+    for i in subs:                                  # the worker's own events are sequential
+        j = names.index("submit_end", i)
+        steps = [a for n, a in ev[i:j] if n == "submit_step"]
+        assert all(st in (1, 2, 3, 4, 5) for st in steps) and ev[j][1] == 0
+    assert t.size == len(names) and np.isfinite(t).all() and 0 < t.max() - t.min() < 60
+
+
 def test_algorithm_module_thread_entry(monkeypatch):
     import threading
     import youth_wire
