@@ -117,7 +117,7 @@ def parse():
     ap.add_argument("--pairs-per-gpu", type=int, default=0,
                     help="> 0: weak scaling with this many pairs per GPU")
     ap.add_argument("--frames", type=int, default=1000, help="sequence workload length")
-    ap.add_argument("--pipeline", type=int, default=0, choices=[0, 1, 2],
+    ap.add_argument("--pipeline", type=int, default=0, choices=[0, 1, 2, 3, 4],
                     help="pairs workload: steps in flight per rank; 2 = two contexts on two "
                          "streams, so step s+1's k_prep / k_icp fill step s's k_icp tail "
                          "(independent batches, each completed inside the timed region); "
