@@ -421,7 +421,11 @@ int youth_icp_track_pending(const youth_icp_ctx* ctx);
  * chip (youth_icp_track_set_batch(ctx, m) plans for m; the default plan at
  * 640x480 holds one pair); the rest one launch per frame.
  * 1 <= n_frames <= YOUTH_TRACK_MAX_BATCH, and at most
- * YOUTH_TRACK_MAX_IN_FLIGHT frames in flight afterwards (EINVAL). */
+ * YOUTH_TRACK_MAX_IN_FLIGHT frames in flight afterwards (EINVAL).
+ * The frames are copied into page-locked staging before the call returns;
+ * from 1 MiB per call the copy is split over the calling thread and the
+ * context's helper threads (3, started by the first such call;
+ * YOUTH_ICP_COPY_THREADS=k sets k, 0 copies on the calling thread only). */
 #define YOUTH_TRACK_MAX_BATCH 8
 int youth_icp_track_submit_batch(youth_icp_ctx* ctx, const int16_t* depth, int n_frames);
 

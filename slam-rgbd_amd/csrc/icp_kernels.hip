@@ -37,6 +37,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -46,6 +47,7 @@
 #include <cstdlib>
 #include <vector>
 
+#include "host_copy.h"
 #include "youth_icp.h"
 
 namespace {
@@ -2544,7 +2546,14 @@ struct youth_icp_ctx {
     int trk_pull_wg = 0;             // YOUTH_ICP_PULL_WG: k_pull_frames workgroups per frame (0: auto)
     int trk_pull_lds = 48 << 10;     // YOUTH_ICP_PULL_LDS: LDS bytes a k_pull_frames workgroup reserves
     int trk_pull_reserve = 32;       // YOUTH_ICP_PULL_RESERVE_CU: CUs a micro-batch plan leaves free
-    bool coop_refuse = false;        // YOUTH_ICP_TEST_REFUSE_COOP=1 (test hook)
+    // staging copies of host frames (track_submit_batch / track_host_sequence):
+    // split over the submitting thread and trk_copy_helpers persistent threads
+    // once a submission holds trk_copy_min bytes (host_copy.h); the pool starts
+    // with the first such submission
+    int trk_copy_helpers = 3;        // YOUTH_ICP_COPY_THREADS: helper threads (0: one thread copies)
+    size_t trk_copy_min = 1u << 20;  // bytes per submission from which the copy is split
+    std::unique_ptr<youth::HostCopyPool> copy_pool;
+    bool coop_refuse = false;       // YOUTH_ICP_TEST_REFUSE_COOP=1 (test hook)
     // occupancy of k_icp_coop<variant, fast, threads> [threads 256?][variant 2 + fast] at npx (LDS)
     int coop_bpc[2][2 * kVariants][kCoopMaxPx + 1] = {};
     int coop_bpc_tall[2 * kVariants] = {};  // the 64 x 80 prep-tile kernel at 10 px per lane
@@ -3471,6 +3480,8 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         if (plds && atoi(plds) >= 0) c->trk_pull_lds = std::min(atoi(plds), 64 << 10);
         const char* pres = getenv("YOUTH_ICP_PULL_RESERVE_CU");
         if (pres && atoi(pres) >= 0) c->trk_pull_reserve = atoi(pres);
+        const char* cpt = getenv("YOUTH_ICP_COPY_THREADS");
+        if (cpt && atoi(cpt) >= 0) c->trk_copy_helpers = std::min(atoi(cpt), 15);
         // test hook (tests/test_gpu_parity.py): every cooperative launch of
         // this context is refused as the runtime would, exercising the
         // persistent fallback of run_iterations
@@ -4171,10 +4182,22 @@ static int track_submit_frames(youth_icp_ctx* c, const int16_t* depth, int m,
     // the copies' stream: the transfer stream (overlaps the launch before),
     // or with YOUTH_ICP_TRACK_COPY=compute the launch stream itself (A/B)
     hipStream_t xs = c->trk_copy_compute ? s : c->xfer;
+    if (!frames) {
+        const size_t fb = N * sizeof(int16_t);
+        if (c->trk_copy_helpers > 0 && (size_t)m * fb >= c->trk_copy_min) {
+            if (!c->copy_pool) c->copy_pool.reset(new youth::HostCopyPool(c->trk_copy_helpers));
+            youth::HostCopyPool::Seg seg[kCoopMaxChain];
+            for (int i = 0; i < m; ++i) seg[i] = {c->trk[qi[i]].pinned, depth + (size_t)i * N, fb};
+            // ~4 pieces per copier per micro-batch: late wake-ups even out
+            const size_t piece = (size_t)m * fb / (4 * (c->trk_copy_helpers + 1));
+            c->copy_pool->run(seg, m, std::max(piece, (size_t)64 << 10));
+        } else {
+            for (int i = 0; i < m; ++i) memcpy(c->trk[qi[i]].pinned, depth + (size_t)i * N, fb);
+        }
+    }
     hipEvent_t waited[kCoopMaxChain];
     int nw = 0;
     for (int i = 0; i < m; ++i) {
-        if (!frames) memcpy(c->trk[qi[i]].pinned, depth + (size_t)i * N, N * sizeof(int16_t));
         const int last = c->trk_dslot_last[d0 + i];
         if (last < 0 || xs == s) continue;
         // the slots of one earlier launch share its event: wait once per event

@@ -1352,15 +1352,21 @@ def test_track_frame_copy_paths_bit_identical(monkeypatch, W, H):
     copy engine (YOUTH_ICP_TRACK_COPY=sdma): the same poses bit for bit, one
     frame per launch and in micro-batches of 4, through track_host_sequence
     (staged copies) and track_submit_pinned (the caller's page-locked
-    buffers)."""
+    buffers).  Also the staging copy of a micro-batch (2.4 MB at 640x480)
+    split over helper threads (the default) against one thread
+    (YOUTH_ICP_COPY_THREADS=0)."""
     frames, _ = youth_synth.sequence(17, 9, W, H)
     K = youth_icp.default_intrinsics(W, H)
     res = {}
-    for path in ("sdma", "pull"):
+    for path in ("sdma", "pull", "pull_1thread"):
         if path == "sdma":
             monkeypatch.setenv("YOUTH_ICP_TRACK_COPY", "sdma")
         else:
             monkeypatch.delenv("YOUTH_ICP_TRACK_COPY", raising=False)
+        if path == "pull_1thread":
+            monkeypatch.setenv("YOUTH_ICP_COPY_THREADS", "0")
+        else:
+            monkeypatch.delenv("YOUTH_ICP_COPY_THREADS", raising=False)
         out = []
         for batch in (1, 4):
             with youth_icp.IcpContext(W, H, 8, K=K) as ctx:
@@ -1382,8 +1388,9 @@ def test_track_frame_copy_paths_bit_identical(monkeypatch, W, H):
                 for b in bufs:
                     b.close()
         res[path] = out
-    for a, b in zip(res["sdma"], res["pull"]):
-        assert np.array_equal(a, b)
+    for other in ("sdma", "pull_1thread"):
+        for a, b in zip(res[other], res["pull"]):
+            assert np.array_equal(a, b), other
     T64, _, _, _ = oracle.align(frames[1], frames[0])
     assert _pose_err(res["pull"][0][0], T64) <= POSE_TOL
 

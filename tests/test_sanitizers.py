@@ -43,3 +43,18 @@ def test_host_threading_under_sanitizer(drivers, kind, env):
     assert "all scenarios passed" in out
     for marker in ("ThreadSanitizer", "AddressSanitizer", "LeakSanitizer", "runtime error"):
         assert marker not in out, out[-4000:]
+
+
+@pytest.mark.parametrize("kind,env", [("tsan", TSAN_ENV), ("asan", ASAN_ENV)], ids=["tsan", "asan"])
+def test_staging_copy_pool_under_sanitizer(drivers, kind, env):
+    """host_copy.h, the tracker's parallel staging copy (track_submit_batch /
+    track_host_sequence): random jobs on 0-4 helpers checked byte for byte,
+    pools driven from several threads, pools torn down idle and right after
+    a job."""
+    r = subprocess.run([os.path.join(drivers, "copy_pool_" + kind)], capture_output=True,
+                       text=True, timeout=300, env={**os.environ, **env})
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "copy pool: all scenarios passed" in out
+    for marker in ("ThreadSanitizer", "AddressSanitizer", "LeakSanitizer", "runtime error"):
+        assert marker not in out, out[-4000:]
