@@ -97,6 +97,20 @@ int oracle_set_spec(int spec)
 
 int oracle_get_spec(void) { return g_spec; }
 
+/* Spec a10 as oracle_align runs it (oracle_set_solve): the block
+ * elimination (the default, what the kernels run) or the round 1-4 LDL^T,
+ * kept so the fixtures' LDL^T poses stay reproducible.  Same threading rule
+ * as g_spec. */
+static int g_solve = ORACLE_SOLVE_BLOCK;
+
+int oracle_set_solve(int mode)
+{
+    if (mode != ORACLE_SOLVE_BLOCK && mode != ORACLE_SOLVE_LDLT) return -1;
+    const int old = g_solve;
+    g_solve = mode;
+    return old;
+}
+
 /* Spec a7 for one source point.  Returns the target index or -1 and, when
  * matched, the transformed point q. */
 static inline int assoc_one(float sx, float sy, float sz, const float T[12],
@@ -287,7 +301,98 @@ void oracle_reduce(const float* sX, const float* sY, const float* sZ,
     memcpy(out, acc, sizeof(acc));
 }
 
+/* Spec a10 (round 5): A x = b by block elimination with 3x3 adjugates,
+ * xi = -x, ONE division on the dependent chain.  With P = A[0..2][0..2]
+ * (rotation), Q = A[0..2][3..5], R = A[3..5][3..5], b = (b1, b2),
+ * C = adj(P):
+ *   detP = P00 C00 + P01 C01 + P02 C02, M = C Q, u = C b1
+ *   S'   = detP R - Q^T M  (detP times the Schur complement)
+ *   y'   = detP b2 - Q^T u
+ *   x2   = adj(S') y' * (1 / det S')
+ *   x1   = C (b1 - Q x2) * (1 / detP)
+ * DEGENERATE (1) iff an LDL^T pivot is <= eps = 1e-12 max diag, tested on the
+ * leading minors by products (pivot j = m_j / m_{j-1}; no division).  Every
+ * a b - c d is fma(a, b, -(c d)); every 3-term dot is
+ * fma(a2, b2, fma(a1, b1, a0 b0)).  The kernels (icp_kernels.hip
+ * solve_block6) perform the same correctly rounded operations in the same
+ * order: xi and the status are bit-identical. */
+static double dd2(double a, double b, double c, double d) { return fma(a, b, -(c * d)); }
+static double dot3(double a0, double b0, double a1, double b1, double a2, double b2)
+{
+    return fma(a2, b2, fma(a1, b1, a0 * b0));
+}
+/* symmetric 3x3 {m00, m01, m02, m11, m12, m22} */
+static void adj3(const double p[6], double c[6])
+{
+    c[0] = dd2(p[3], p[5], p[4], p[4]);
+    c[1] = dd2(p[2], p[4], p[1], p[5]);
+    c[2] = dd2(p[1], p[4], p[2], p[3]);
+    c[3] = dd2(p[0], p[5], p[2], p[2]);
+    c[4] = dd2(p[1], p[2], p[0], p[4]);
+    c[5] = dd2(p[0], p[3], p[1], p[1]);
+}
+static void symv3(const double c[6], const double v[3], double o[3])
+{
+    o[0] = dot3(c[0], v[0], c[1], v[1], c[2], v[2]);
+    o[1] = dot3(c[1], v[0], c[3], v[1], c[4], v[2]);
+    o[2] = dot3(c[2], v[0], c[4], v[1], c[5], v[2]);
+}
+
 int oracle_solve(const double neq[ORACLE_NEQ], double xi[6])
+{
+    for (int i = 0; i < 6; ++i) xi[i] = 0.0;
+    if (!(neq[28] >= 6.0)) return 2;
+    static const int diag[6] = {0, 6, 11, 15, 18, 20};
+    double maxd = 0.0;
+    for (int a = 0; a < 6; ++a)
+        if (neq[diag[a]] > maxd) maxd = neq[diag[a]];
+    if (!(maxd > 0.0)) return 1;
+    const double eps = 1e-12 * maxd;
+    const double P[6] = {neq[0], neq[1], neq[2], neq[6], neq[7], neq[11]};
+    const double R[6] = {neq[15], neq[16], neq[17], neq[18], neq[19], neq[20]};
+    const double Q[3][3] = {{neq[3], neq[4], neq[5]}, {neq[8], neq[9], neq[10]},
+                            {neq[12], neq[13], neq[14]}};
+    const double b1[3] = {neq[21], neq[22], neq[23]}, b2[3] = {neq[24], neq[25], neq[26]};
+    double C[6], E[6], S[6], M[3][3], u[3], y[3], v[3], x2[3], w[3];
+    adj3(P, C);
+    const double detP = dot3(P[0], C[0], P[1], C[1], P[2], C[2]);
+    for (int j = 0; j < 3; ++j) {  /* M = C Q, column by column */
+        const double q[3] = {Q[0][j], Q[1][j], Q[2][j]};
+        double o[3];
+        symv3(C, q, o);
+        for (int i = 0; i < 3; ++i) M[i][j] = o[i];
+    }
+    symv3(C, b1, u);
+    static const int si[6] = {0, 0, 0, 1, 1, 2}, sj[6] = {0, 1, 2, 1, 2, 2};
+    for (int e = 0; e < 6; ++e) {  /* S' upper triangle: detP R[i][j] - (Q^T M)[i][j] */
+        const int i = si[e], j = sj[e];
+        S[e] = fma(detP, R[e], -dot3(Q[0][i], M[0][j], Q[1][i], M[1][j], Q[2][i], M[2][j]));
+    }
+    for (int j = 0; j < 3; ++j)
+        y[j] = fma(detP, b2[j], -dot3(Q[0][j], u[0], Q[1][j], u[1], Q[2][j], u[2]));
+    adj3(S, E);
+    const double detS = dot3(S[0], E[0], S[1], E[1], S[2], E[2]);
+    const double epsP = eps * detP;
+    /* pivots: P00, C22/P00, detP/C22, S'00/detP, E22/(detP S'00), detS/(detP E22) */
+    if (!(P[0] > eps) || !(C[5] > eps * P[0]) || !(detP > eps * C[5]) || !(S[0] > epsP) ||
+        !(E[5] > epsP * S[0]) || !(detS > epsP * E[5]))
+        return 1;
+    const double rS = 1.0 / detS, rP = 1.0 / detP;
+    symv3(E, y, v);
+    for (int i = 0; i < 3; ++i) x2[i] = v[i] * rS;
+    for (int i = 0; i < 3; ++i) w[i] = b1[i] - dot3(Q[i][0], x2[0], Q[i][1], x2[1], Q[i][2], x2[2]);
+    symv3(C, w, v);
+    for (int i = 0; i < 3; ++i) {
+        xi[i] = -(v[i] * rP);
+        xi[3 + i] = -x2[i];
+    }
+    return 0;
+}
+
+/* Round 1-4 spec a10: LDL^T of A xi = -b (right-looking on the GPU, the
+ * same per-element operations).  Kept for the fixtures' LDL^T poses
+ * (the T64_ldlt field of the tests/golden pair fixtures) and the solve A/B. */
+int oracle_solve_ldlt(const double neq[ORACLE_NEQ], double xi[6])
 {
     for (int i = 0; i < 6; ++i) xi[i] = 0.0;
     if (!(neq[28] >= 6.0)) return 2;
@@ -433,7 +538,7 @@ static int align_ws(const int16_t* src, const int16_t* dst, int W, int H,
             stats[2 * it + 0] = neq[28];
             stats[2 * it + 1] = neq[27];
         }
-        const int st = oracle_solve(neq, xi);
+        const int st = g_solve == ORACLE_SOLVE_LDLT ? oracle_solve_ldlt(neq, xi) : oracle_solve(neq, xi);
         status |= st;
         if (st == 0) {
             oracle_se3_exp(xi, E);

@@ -19,7 +19,7 @@
  * PARITY UNPINNED for everything after back-projection: the reference has no
  * ICP (its pose maths is inside un-vendored ORB-SLAM3,
  * SLAM.cpp:54, version unpinned, feature-based).  Normals, projective
- * association, point-to-plane Jacobian, 6x6 reduction, LDL^T solve and the
+ * association, point-to-plane Jacobian, 6x6 reduction, 6x6 solve and the
  * SE(3) update follow this build's own spec (SURVEY.md §8a rows a6-a10,
  * DESIGN.md §2), checked here against numpy/scipy and known-motion recovery.
  *
@@ -123,9 +123,20 @@ void oracle_reduce(const float* sX, const float* sY, const float* sZ,
                    int W, int H, const oracle_intrinsics* K, const float T[12],
                    float dist_thresh, double out[ORACLE_NEQ]);
 
-/* LDL^T solve of A xi = -b (spec a10).  Returns 0, or status bits
- * (1 = singular pivot, 2 = fewer than 6 correspondences); xi zeroed then. */
+/* Solve of A xi = -b (spec a10, round 5): block (3+3) elimination with 3x3
+ * adjugates, one division on the dependent chain.  Returns 0,
+ * or status bits (1 = an LDL^T pivot <= 1e-12 max diag, tested on the
+ * leading minors; 2 = fewer than 6 correspondences); xi zeroed then. */
 int oracle_solve(const double neq[ORACLE_NEQ], double xi[6]);
+/* The round 1-4 spec a10: LDL^T, one IEEE reciprocal per pivot.  Not used by
+ * oracle_align unless oracle_set_solve(ORACLE_SOLVE_LDLT); kept for the
+ * fixtures' T64_ldlt poses. */
+int oracle_solve_ldlt(const double neq[ORACLE_NEQ], double xi[6]);
+/* Which of the two oracle_align uses (the kernels run the block form only);
+ * returns the previous mode, -1 for an unknown one. */
+#define ORACLE_SOLVE_BLOCK 0
+#define ORACLE_SOLVE_LDLT 1
+int oracle_set_solve(int mode);
 
 /* SE(3) exponential of xi = (omega, upsilon), 4x4 row-major fp64. */
 void oracle_se3_exp(const double xi[6], double E[16]);

@@ -47,6 +47,10 @@ def load_library() -> ctypes.CDLL:
     lib.oracle_reduce.argtypes = [PF] * 9 + [c_int, c_int, PK, PF, c_float, PD]
     lib.oracle_solve.argtypes = [PD, PD]
     lib.oracle_solve.restype = c_int
+    lib.oracle_solve_ldlt.argtypes = [PD, PD]
+    lib.oracle_solve_ldlt.restype = c_int
+    lib.oracle_set_solve.argtypes = [c_int]
+    lib.oracle_set_solve.restype = c_int
     lib.oracle_se3_exp.argtypes = [PD, PD]
     lib.oracle_align.argtypes = [P16, P16, c_int, c_int, PK, c_int, c_float, PD, PD, PF, PD]
     lib.oracle_align.restype = c_int
@@ -235,9 +239,35 @@ def reduce(src, dst, T12, K=None, dist_thresh: float = 0.10):
 
 
 def solve(neq):
+    """Spec a10: block elimination with 3x3 adjugates (oracle_solve)."""
     n = np.ascontiguousarray(neq, np.float64)
     xi = np.zeros(6, np.float64)
     st = load_library().oracle_solve(_p(n, c_double), _p(xi, c_double))
+    return xi, st
+
+
+class solve_mode:
+    """Context manager selecting the solve oracle_align runs: ``with
+    oracle.solve_mode("ldlt"): ...`` (the round 1-4 spec a10, for the
+    fixtures' T64_ldlt poses); "block" is the default and what the kernels
+    run."""
+
+    def __init__(self, name):
+        self.code = {"block": 0, "ldlt": 1}[name]
+
+    def __enter__(self):
+        self.old = load_library().oracle_set_solve(self.code)
+        return self
+
+    def __exit__(self, *exc):
+        load_library().oracle_set_solve(self.old)
+
+
+def solve_ldlt(neq):
+    """The round 1-4 spec a10 (LDL^T), for the fixtures' T64_ldlt poses."""
+    n = np.ascontiguousarray(neq, np.float64)
+    xi = np.zeros(6, np.float64)
+    st = load_library().oracle_solve_ldlt(_p(n, c_double), _p(xi, c_double))
     return xi, st
 
 

@@ -817,54 +817,109 @@ __global__ __launch_bounds__(kPrepThreads) void k_prep(const int16_t* __restrict
 }
 
 // ----------------------------------------------------------------- k_solve --
-// LDL^T + SE(3) exp, same algorithm and evaluation order as oracle_solve /
-// oracle_se3_exp (oracle/icp_oracle.c).
-__device__ int solve6(const double* neq, double xi[6])
+// Spec a10 (round 5): A x = b by block elimination with 3x3 adjugates, xi =
+// -x; the same correctly rounded operations in the same order as
+// oracle_solve (oracle/icp_oracle.c), so xi and the status are bit-identical.
+// With P = A[0..2][0..2] (rotation), Q = A[0..2][3..5], R = A[3..5][3..5],
+// b = (b1, b2), C = adj(P):
+//   detP = P00 C00 + P01 C01 + P02 C02, M = C Q, u = C b1
+//   S' = detP R - Q^T M (detP times the Schur complement), y' = detP b2 - Q^T u
+//   x2 = adj(S') y' * (1 / det S'),  x1 = C (b1 - Q x2) * (1 / detP)
+// ONE division on the dependent chain (1 / detP runs beside it) and no value
+// crosses lanes, against LDL^T's six dependent reciprocals and lane
+// broadcasts (tools/solvebench).  The rotation block goes first,
+// as LDL^T's pivot order does: eliminating the translation block first was
+// faster on paper but 2-3x more sensitive to the sums' last bits on
+// ill-conditioned frames.  DEGENERATE iff an LDL^T pivot is
+// <= 1e-12 max diag, tested on the leading minors by products.
+__device__ __forceinline__ double dd2(double a, double b, double c, double d)
 {
+    return fma(a, b, -(c * d));  // a b - c d
+}
+__device__ __forceinline__ double dot3(double a0, double b0, double a1, double b1, double a2,
+                                       double b2)
+{
+    return fma(a2, b2, fma(a1, b1, a0 * b0));
+}
+// symmetric 3x3 {m00, m01, m02, m11, m12, m22}: adjugate, matrix-vector
+__device__ __forceinline__ void adj3(const double* p, double* c)
+{
+    c[0] = dd2(p[3], p[5], p[4], p[4]);
+    c[1] = dd2(p[2], p[4], p[1], p[5]);
+    c[2] = dd2(p[1], p[4], p[2], p[3]);
+    c[3] = dd2(p[0], p[5], p[2], p[2]);
+    c[4] = dd2(p[1], p[2], p[0], p[4]);
+    c[5] = dd2(p[0], p[3], p[1], p[1]);
+}
+__device__ __forceinline__ void symv3(const double* c, const double* v, double* o)
+{
+    o[0] = dot3(c[0], v[0], c[1], v[1], c[2], v[2]);
+    o[1] = dot3(c[1], v[0], c[3], v[1], c[4], v[2]);
+    o[2] = dot3(c[2], v[0], c[4], v[1], c[5], v[2]);
+}
+// neq wave-uniform (LDS or registers); every lane computes everything, so no
+// value crosses lanes.  xi is zeroed on a nonzero status.
+__device__ __forceinline__ int solve_block6(const double* neq, double xi[6])
+{
+#pragma unroll
     for (int i = 0; i < 6; ++i) xi[i] = 0.0;
     if (!(neq[28] >= 6.0)) return YOUTH_STATUS_FEW_MATCHES;
-    double A[6][6];
-    int k = 0;
-    for (int a = 0; a < 6; ++a)
-        for (int b = a; b < 6; ++b) {
-            A[a][b] = neq[k];
-            A[b][a] = neq[k];
-            ++k;
-        }
-    double maxd = 0.0;
-    for (int a = 0; a < 6; ++a)
-        if (A[a][a] > maxd) maxd = A[a][a];
+    double maxd = 0.0;  // the diagonal, in order (a, a) = 0, 6, 11, 15, 18, 20
+    maxd = neq[0] > maxd ? neq[0] : maxd;
+    maxd = neq[6] > maxd ? neq[6] : maxd;
+    maxd = neq[11] > maxd ? neq[11] : maxd;
+    maxd = neq[15] > maxd ? neq[15] : maxd;
+    maxd = neq[18] > maxd ? neq[18] : maxd;
+    maxd = neq[20] > maxd ? neq[20] : maxd;
     if (!(maxd > 0.0)) return YOUTH_STATUS_DEGENERATE;
     const double eps = 1e-12 * maxd;
-    double L[6][6], D[6], Dinv[6];
-    for (int i = 0; i < 6; ++i)
-        for (int j = 0; j < 6; ++j) L[i][j] = 0.0;
-    for (int j = 0; j < 6; ++j) {
-        double d = A[j][j];
-        for (int m = 0; m < j; ++m) d -= (L[j][m] * L[j][m]) * D[m];
-        if (!(d > eps)) return YOUTH_STATUS_DEGENERATE;
-        D[j] = d;
-        Dinv[j] = 1.0 / d;  /* one divide per pivot; every use multiplies */
-        L[j][j] = 1.0;
-        for (int i = j + 1; i < 6; ++i) {
-            double s = A[i][j];
-            for (int m = 0; m < j; ++m) s -= (L[i][m] * L[j][m]) * D[m];
-            L[i][j] = s * Dinv[j];
-        }
+    const double P[6] = {neq[0], neq[1], neq[2], neq[6], neq[7], neq[11]};
+    const double R[6] = {neq[15], neq[16], neq[17], neq[18], neq[19], neq[20]};
+    const double Q[3][3] = {{neq[3], neq[4], neq[5]}, {neq[8], neq[9], neq[10]},
+                            {neq[12], neq[13], neq[14]}};
+    const double b1[3] = {neq[21], neq[22], neq[23]}, b2[3] = {neq[24], neq[25], neq[26]};
+    double C[6], E[6], S[6], M[3][3], u[3], y[3], v[3], x2[3], w[3];
+    adj3(P, C);
+    const double detP = dot3(P[0], C[0], P[1], C[1], P[2], C[2]);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {  // M = C Q, column by column
+        const double q[3] = {Q[0][j], Q[1][j], Q[2][j]};
+        double o[3];
+        symv3(C, q, o);
+        M[0][j] = o[0];
+        M[1][j] = o[1];
+        M[2][j] = o[2];
     }
-    double y[6], x[6];
-    for (int i = 0; i < 6; ++i) {
-        double s = -neq[21 + i];
-        for (int m = 0; m < i; ++m) s -= L[i][m] * y[m];
-        y[i] = s;
+    symv3(C, b1, u);
+    // S' upper triangle (i <= j): detP R[i][j] - (Q^T M)[i][j]
+    S[0] = fma(detP, R[0], -dot3(Q[0][0], M[0][0], Q[1][0], M[1][0], Q[2][0], M[2][0]));
+    S[1] = fma(detP, R[1], -dot3(Q[0][0], M[0][1], Q[1][0], M[1][1], Q[2][0], M[2][1]));
+    S[2] = fma(detP, R[2], -dot3(Q[0][0], M[0][2], Q[1][0], M[1][2], Q[2][0], M[2][2]));
+    S[3] = fma(detP, R[3], -dot3(Q[0][1], M[0][1], Q[1][1], M[1][1], Q[2][1], M[2][1]));
+    S[4] = fma(detP, R[4], -dot3(Q[0][1], M[0][2], Q[1][1], M[1][2], Q[2][1], M[2][2]));
+    S[5] = fma(detP, R[5], -dot3(Q[0][2], M[0][2], Q[1][2], M[1][2], Q[2][2], M[2][2]));
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+        y[j] = fma(detP, b2[j], -dot3(Q[0][j], u[0], Q[1][j], u[1], Q[2][j], u[2]));
+    adj3(S, E);
+    const double detS = dot3(S[0], E[0], S[1], E[1], S[2], E[2]);
+    const double epsP = eps * detP;
+    // pivots P00, C22/P00, detP/C22, S'00/detP, E22/(detP S'00), detS/(detP E22)
+    const bool ok = (P[0] > eps) & (C[5] > eps * P[0]) & (detP > eps * C[5]) & (S[0] > epsP) &
+                    (E[5] > epsP * S[0]) & (detS > epsP * E[5]);
+    if (!ok) return YOUTH_STATUS_DEGENERATE;
+    const double rS = 1.0 / detS, rP = 1.0 / detP;
+    symv3(E, y, v);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) x2[i] = v[i] * rS;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) w[i] = b1[i] - dot3(Q[i][0], x2[0], Q[i][1], x2[1], Q[i][2], x2[2]);
+    symv3(C, w, v);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        xi[i] = -(v[i] * rP);
+        xi[3 + i] = -x2[i];
     }
-    for (int i = 0; i < 6; ++i) y[i] = y[i] * Dinv[i];
-    for (int i = 5; i >= 0; --i) {
-        double s = y[i];
-        for (int m = 5; m > i; --m) s -= L[m][i] * x[m];
-        x[i] = s;
-    }
-    for (int i = 0; i < 6; ++i) xi[i] = x[i];
     return 0;
 }
 
@@ -917,84 +972,17 @@ __device__ void se3_exp_left(const double xi[6], double* T)
     for (int i = 0; i < 12; ++i) T[i] = O[i];
 }
 
-// Spec a10 by ONE wave (all 64 lanes call it): solve6 + se3_exp_left with
-// their per-element operations and order (bit-identical results), spread
-// over lanes because a lone lane pays the wave's full issue cost for every
-// fp64 instruction (~2.2 us per iteration on one lane, tools/coopbench):
-//   * lane i < 6 owns row i of A and L: column j of the factorisation is one
-//     step (the pivot d_j and every L[i][j] together), L[j][m] and d_j are
-//     broadcast with v_readlane;
-//   * forward / back substitution: lane i owns y_i / x_i and subtracts
-//     L[i][m] y_m (m increasing) / L[m][i] x_m (m decreasing) as each
-//     becomes final;
-//   * lane l < 12 computes output entry (l / 4, l % 4) of exp(xi^) T.
-// neq (LDS, kNeq): the pair's sums; T64 (LDS, 12): pose in/out; T32 (LDS,
-// 12): fp32 copy out; Lsh (LDS, 36): scratch.  Returns the status bits; the
-// pose is updated only when they are 0.
-__device__ __forceinline__ int tri6(int a, int b)  // upper-triangle index, a <= b
+// Spec a10 by ONE wave (all 64 lanes call it): solve_block6 in every lane
+// (wave-uniform, no cross-lane traffic), then se3_exp_left with its
+// per-element operations and order, lane l < 12 computing output entry
+// (l / 4, l % 4) of exp(xi^) T.  neq (LDS, kNeq): the pair's sums; T64 (LDS,
+// 12): pose in/out; T32 (LDS, 12): fp32 copy out.  Returns the status bits;
+// the pose is updated only when they are 0.
+__device__ __forceinline__ int solve_update_wave(const double* neq, double* T64, float* T32, int lane)
 {
-    return a * 6 - (a * (a - 1)) / 2 + (b - a);
-}
-
-__device__ __forceinline__ int solve_update_wave(const double* neq, double* T64, float* T32,
-                                                double* Lsh, int lane)
-{
-    if (!(neq[28] >= 6.0)) return YOUTH_STATUS_FEW_MATCHES;
-    const int i = lane < 6 ? lane : 5;
-    double maxd = 0.0;
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-        const double da = neq[tri6(a, a)];
-        if (da > maxd) maxd = da;
-    }
-    if (!(maxd > 0.0)) return YOUTH_STATUS_DEGENERATE;
-    const double eps = 1e-12 * maxd;
-    // LDL^T right-looking: lane i holds row i, S[j] = A[i][j] minus the
-    // terms of the columns done so far.  Every element receives the same
-    // subtractions in the same order (m increasing) as the left-looking
-    // spec (solve6), so the results are bit-identical; but column m's
-    // updates of the later columns and its forward-substitution step are
-    // independent of column m+1's pivot divide and overlap it.  No early
-    // exit inside the loop (one basic block): a failed pivot is flagged and
-    // returned after it (nothing is stored before).
-    double S[6], Lr[6], D[6], Dinv[6];
-#pragma unroll
-    for (int j = 0; j < 6; ++j) S[j] = neq[i <= j ? tri6(i, j) : tri6(j, i)];
-    // forward: y_i = (-b_i - sum_{m<i} L[i][m] y_m) / d_i, step m right after column m
-    double y = -neq[21 + i];
-    bool bad = false;
-#pragma unroll
-    for (int m = 0; m < 6; ++m) {
-        const double d = readlane64(S[m], m);
-        bad |= !(d > eps);
-        D[m] = d;
-        Dinv[m] = 1.0 / d;  // one divide per pivot; every use multiplies
-        Lr[m] = lane > m ? S[m] * Dinv[m] : (lane == m ? 1.0 : 0.0);
-#pragma unroll
-        for (int j = m + 1; j < 6; ++j) S[j] -= (Lr[m] * readlane64(Lr[m], j)) * D[m];
-        const double ym = readlane64(y, m);
-        y = lane > m ? y - Lr[m] * ym : y;
-    }
-    if (bad) return YOUTH_STATUS_DEGENERATE;
-    double dinv = Dinv[0];
-#pragma unroll
-    for (int j = 1; j < 6; ++j) dinv = i == j ? Dinv[j] : dinv;
-    y = y * dinv;
-    // back: x_i = y_i - sum_{m>i} L[m][i] x_m, m decreasing (column i of L via LDS)
-    if (lane < 6) {
-#pragma unroll
-        for (int j = 0; j < 6; ++j) Lsh[lane * 6 + j] = Lr[j];
-    }
-    double x = y;
-#pragma unroll
-    for (int m = 5; m >= 0; --m) {
-        const double xm = readlane64(x, m);
-        const double Lmi = Lsh[m * 6 + i];
-        x = lane < m ? x - Lmi * xm : x;
-    }
     double xi[6];
-#pragma unroll
-    for (int m = 0; m < 6; ++m) xi[m] = readlane64(x, m);
+    const int st = solve_block6(neq, xi);
+    if (st) return st;
 
     // T <- exp(xi^) T (se3_exp_left), one output entry per lane
     const double wx = xi[0], wy = xi[1], wz = xi[2];
@@ -1048,9 +1036,9 @@ __device__ __forceinline__ int solve_update_wave(const double* neq, double* T64,
 // pixel loop (128-VGPR budget), then reloaded from scratch on the pair's
 // critical path.  A call keeps its registers to itself.
 __device__ __attribute__((noinline)) int solve_update_wave_call(const double* neq, double* T64,
-                                                                float* T32, double* Lsh, int lane)
+                                                                float* T32, int lane)
 {
-    return solve_update_wave(neq, T64, T32, Lsh, lane);
+    return solve_update_wave(neq, T64, T32, lane);
 }
 
 // Sum the nblk partials of pair p in a fixed order: lanes 0..28 take the
@@ -1076,7 +1064,7 @@ __device__ __forceinline__ void solve_update(const double* neq, double* T64, flo
                                              int32_t* status)
 {
     double xi[6];
-    const int st = solve6(neq, xi);
+    const int st = solve_block6(neq, xi);
     double T[16];
     for (int i = 0; i < 16; ++i) T[i] = T64[i];
     if (st == 0) se3_exp_left(xi, T);
@@ -1869,7 +1857,6 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
     __shared__ double red[kRedThreads / 64][kNeq];
     __shared__ double colsum[kSumCols][kPartStride];
     __shared__ double sh_neq[kNeq];
-    __shared__ double sh_L[36];
     __shared__ double sh_T64[12];
     __shared__ float sh_T32n[12];
     __shared__ int sh_item;
@@ -1967,7 +1954,7 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
                     is.stats[((size_t)p * is.iters + k) * 2 + 0] = readlane64(tsum, 28);
                     is.stats[((size_t)p * is.iters + k) * 2 + 1] = readlane64(tsum, 27);
                 }
-                const int st = solve_update_wave_call(sh_neq, sh_T64, sh_T32n, sh_L, lane);
+                const int st = solve_update_wave_call(sh_neq, sh_T64, sh_T32n, lane);
                 if (st && lane == 0)
                     __hip_atomic_fetch_or(is.status + p, st, __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT);
@@ -2147,7 +2134,6 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
     __shared__ double red[kThreads / 64][kNeq];
     __shared__ double colsum[kSumCols][kPartStride];
     __shared__ double sh_neq[kNeq];
-    __shared__ double sh_L[36];
     __shared__ double sh_T64[12];
     __shared__ float sh_T[12];
     __shared__ int sh_stop;
@@ -2365,7 +2351,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
                 cs.stats[((size_t)p * cs.iters + k) * 2 + 1] = readlane64(tsum, 27);
             }
             COOP_MARK(k, 8);
-            st_acc |= solve_update_wave(sh_neq, sh_T64, sh_T, sh_L, lane);
+            st_acc |= solve_update_wave(sh_neq, sh_T64, sh_T, lane);
             COOP_MARK(k, 9);
             COOP_MARK(k, 10);
         }

@@ -15,6 +15,12 @@ Provenance, case by case:
     fma spec existed (identical to git 1041b06^:tests/golden/); running this
     script regenerates them with today's oracle and leaves their arrays
     equal (tests/test_oracle.py checks that without writing).
+  * Round 5 changed spec a10's solve (LDL^T -> block elimination with 3x3
+    adjugates).  T64 / T32 / status / stats / idx_final
+    (pairs) and T_rel (sequences) are the block solve's; the round-1 LDL^T
+    results stay in the files verbatim as T64_ldlt / T32_ldlt and T_rel_ldlt
+    (the oracle reproduces them in oracle.solve_mode("ldlt")).  Everything
+    before the solve (xyz, normals, association, neq) is unchanged.
   * fma/pair_* / fma/seq_* — the same cases in the opt-in fma spec
     (ORACLE_SPEC_FMA, `--fma`).  The reference has no ICP, so
     these pin this build's own spec against regressions: "parity unpinned"
@@ -62,6 +68,8 @@ def make_pair_case(name, W, H, index, iters=10, dist=0.10, out=HERE):
     idx0 = oracle.associate(src, dst, I12, K, dist)
     neq0 = oracle.reduce(src, dst, I12, K, dist)
     T64, T32, st, stats = oracle.align(src, dst, K, iters, dist)
+    with oracle.solve_mode("ldlt"):
+        T64l, T32l, _, _ = oracle.align(src, dst, K, iters, dist)
     idxF = oracle.associate(src, dst, T32, K, dist)
     np.savez_compressed(
         os.path.join(out, name + ".npz"), src=src, dst=dst,
@@ -69,7 +77,8 @@ def make_pair_case(name, W, H, index, iters=10, dist=0.10, out=HERE):
         iters=np.int32(iters), dist_thresh=np.float32(dist), T_gt=Tgt[0],
         src_xyz=np.stack([sX, sY, sZ]), dst_xyz=np.stack([tX, tY, tZ]),
         dst_nrm=np.stack([nX, nY, nZ]), idx_identity=idx0, neq_identity=neq0,
-        T64=T64, T32=T32, status=np.int32(st), stats=stats, idx_final=idxF)
+        T64=T64, T32=T32, status=np.int32(st), stats=stats, idx_final=idxF,
+        T64_ldlt=T64l, T32_ldlt=T32l)
     print(f"{name}: status={st} matches0={int((idx0 >= 0).sum())} "
           f"final count={stats[-1, 0]:.0f}")
 
@@ -82,14 +91,16 @@ def _yk(K):
 def make_seq_case(name, W, H, n_frames, iters=10, dist=0.10, out=HERE):
     K = scaled_K(W, H)
     frames, Twc = youth_synth.sequence(0, n_frames, W, H, K=_yk(K))
-    rel = []
+    rel, rel_l = [], []
     for k in range(n_frames - 1):
         T64, T32, st, _ = oracle.align(frames[k + 1], frames[k], K, iters, dist)
         rel.append(T64)
+        with oracle.solve_mode("ldlt"):
+            rel_l.append(oracle.align(frames[k + 1], frames[k], K, iters, dist)[0])
     np.savez_compressed(os.path.join(out, name + ".npz"), frames=frames,
                         K=np.array([K.fx, K.fy, K.cx, K.cy, K.depth_scale], np.float32),
                         iters=np.int32(iters), dist_thresh=np.float32(dist), T_wc=Twc,
-                        T_rel=np.stack(rel))
+                        T_rel=np.stack(rel), T_rel_ldlt=np.stack(rel_l))
     print(f"{name}: {n_frames} frames")
 
 

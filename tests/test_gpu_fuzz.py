@@ -142,7 +142,11 @@ def test_tiny_and_ragged_frames_every_path(W, H, monkeypatch):
     the stage kernel's association bit-exact and sums within rel 1e-11 of the
     oracle; full aligns through the persistent kernel (2 pairs) and
     k_icp_coop (1 pair) with equal per-iteration counts and statuses, poses
-    within 1e-9."""
+    within 1e-9 + 4e-16 cond(A): the GPU and the oracle add the same exact
+    products in different fp64 orders (~1e-16 relative), and the one-row /
+    one-column frames' normal equations have cond(A) up to ~3e8, which the
+    solve (any exact solve: round 1-4's LDL^T was as sensitive) amplifies.
+    cond(A) is taken at the oracle's final pose."""
     rng = np.random.default_rng(0x7111 + W * 131 + H)
     src, dst, _ = youth_synth.pairs(96, 2, W, H)
     ds, dd = torch.from_numpy(src).cuda(), torch.from_numpy(dst).cuda()
@@ -173,7 +177,11 @@ def test_tiny_and_ragged_frames_every_path(W, H, monkeypatch):
                                                     n_threads=n, want_stats=True)
         assert np.array_equal(st, sto), (plan["kernel"], st, sto)
         assert np.array_equal(cnt, stats[..., 0]), (plan["kernel"], cnt, stats[..., 0])
-        ok = st == 0
-        if ok.any():
-            err = float(np.abs(np.asarray(T64)[ok][..., :3, :4] - np.asarray(To)[ok][..., :3, :4]).max())
-            assert err <= 1e-9, (plan["kernel"], err)
+        for p in np.flatnonzero(st == 0):
+            err = float(np.abs(np.asarray(T64)[p][:3, :4] - np.asarray(To)[p][:3, :4]).max())
+            neq = oracle.reduce(src[p], dst[p], np.asarray(To)[p][:3].astype(np.float32), Ko)
+            A = np.zeros((6, 6))
+            A[np.triu_indices(6)] = neq[:21]
+            A = A + np.triu(A, 1).T
+            bound = 1e-9 + 4e-16 * np.linalg.cond(A)
+            assert err <= bound, (plan["kernel"], p, err, bound)

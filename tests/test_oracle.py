@@ -84,6 +84,37 @@ def test_solve_matches_numpy():
         assert np.abs(xi - np.linalg.solve(A, -b)).max() < 1e-10
 
 
+def test_block_solve_against_ldlt():
+    """Spec a10 changed in round 5 from LDL^T to block elimination with 3x3
+    adjugates (one division on the chain).  On systems built
+    like the ICP's (A = J^T J of rotation-and-translation Jacobians) both
+    solve A xi = -b to ~1e-15 relative, and their DEGENERATE tests (LDL^T
+    pivots vs the block form's leading-minor products) agree on full-rank and
+    rank-deficient systems away from the 1e-12 threshold."""
+    rng = np.random.default_rng(11)
+    for k in range(200):
+        n = 50 + k
+        p = rng.normal(size=(n, 3)) * 2.0
+        nrm = rng.normal(size=(n, 3))
+        nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+        J = np.hstack([np.cross(p, nrm), nrm])
+        if k % 4 == 3:
+            J[:, 3:] = J[:, 3:] * 0 + nrm[0]             # one normal: rank-deficient
+        r = rng.normal(size=n) * 1e-3
+        A, b = J.T @ J, J.T @ r
+        neq = np.zeros(29)
+        neq[:21] = A[np.triu_indices(6)]
+        neq[21:27] = b
+        neq[28] = n
+        xb, sb = oracle.solve(neq)
+        xl, sl = oracle.solve_ldlt(neq)
+        assert sb == sl, k
+        if sb == 0:
+            ref = np.linalg.solve(A, -b)
+            assert np.abs(xb - ref).max() <= 1e-12 * np.abs(ref).max(), k
+            assert np.abs(xb - xl).max() <= 1e-12 * np.abs(ref).max(), k
+
+
 def test_solve_degenerate_cases():
     neq = np.zeros(29)
     neq[28] = 3
@@ -230,8 +261,9 @@ def test_survey_spec_reproduces_round1_fixtures(name):
     reproduces, bit for bit, the fixtures the round-1 oracle committed before
     the fma spec existed (git 1041b06^:tests/golden/, the default fixtures
     again): association at identity and at the final pose, the identity
-    normal equations, per-iteration stats and the final pose.  So the survey
-    spec is a fixed point the kernels did not move."""
+    normal equations, per-iteration stats and the final pose (the final fp64
+    pose of the round-5 solve: the round-1 one is T64_ldlt, checked below).
+    So the survey spec is a fixed point the kernels did not move."""
     g = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
     K, d, it = _K(g["K"]), float(g["dist_thresh"]), int(g["iters"])
     I12 = np.eye(4, dtype=np.float32)[:3]
@@ -258,6 +290,31 @@ def test_survey_spec_reproduces_round1_fixtures(name):
     assert np.array_equal(T64f, gf["T64"]) and np.array_equal(statsf, gf["stats"])
     assert np.array_equal(neqf.view(np.uint64), gf["neq_identity"].view(np.uint64))
     assert np.array_equal(idxf, gf["idx_final"])
+
+
+@pytest.mark.parametrize("sub", ["", "fma"])
+def test_round1_ldlt_poses_kept_and_block_solve_close(sub):
+    """The fixtures keep the round-1 LDL^T poses verbatim (T64_ldlt, T32_ldlt,
+    T_rel_ldlt): the oracle in solve_mode("ldlt") still reproduces them bit
+    for bit, and the round-5 block solve (T64, T_rel) lands within 1e-15 of
+    them with the same fp32 pose and status (the solve is the only change)."""
+    base = os.path.join(GOLDEN, sub)
+    spec = "fma" if sub else "survey"
+    for name in PAIR_CASES:
+        g = np.load(os.path.join(base, name + ".npz"), allow_pickle=False)
+        K, d, it = _K(g["K"]), float(g["dist_thresh"]), int(g["iters"])
+        with oracle.spec(spec), oracle.solve_mode("ldlt"):
+            T64, T32, st, _ = oracle.align(g["src"], g["dst"], K, it, d)
+        assert np.array_equal(T64, g["T64_ldlt"]) and np.array_equal(T32, g["T32_ldlt"])
+        assert st == int(g["status"]) and np.array_equal(g["T32"], g["T32_ldlt"])
+        assert np.abs(g["T64"] - g["T64_ldlt"]).max() < 1e-15
+    g = np.load(os.path.join(base, "seq_128x96.npz"), allow_pickle=False)
+    K, d, it = _K(g["K"]), float(g["dist_thresh"]), int(g["iters"])
+    f = g["frames"]
+    with oracle.spec(spec), oracle.solve_mode("ldlt"):
+        for k in range(f.shape[0] - 1):
+            assert np.array_equal(oracle.align(f[k + 1], f[k], K, it, d)[0], g["T_rel_ldlt"][k])
+    assert np.abs(g["T_rel"] - g["T_rel_ldlt"]).max() < 1e-15
 
 
 def test_survey_spec_reproduces_round1_sequence_fixture():

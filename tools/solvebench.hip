@@ -1,146 +1,27 @@
-// solvebench — latency of the one-wave spec-a10 solve on ONE wave, the
-// k_icp_coop critical path (tools/coopbench: LDL^T ~1.8 us of an 8.7 us
-// iteration).  Each kernel runs `reps` dependent solves (the pose feeds the
-// next) and reports s_memrealtime ns per solve; every variant's poses must
-// equal production's bitwise.
-// Build: make -C tools solvebench        Run (GPU box): tools/solvebench
+// solvebench — latency of the one-wave spec-a10 solve + SE(3) update on ONE
+// wave, the k_icp_coop critical path (tools/coopbench), and bitwise checks of
+// the device solve against the CPU oracle.  Each timing kernel runs `reps`
+// dependent solves (the pose feeds the next) and reports s_memrealtime ns per
+// solve.  Variants: production solve_update_wave (block elimination,
+// rotation block first, round 5); the round 1-4 LDL^T (right-looking, lane
+// i holds row i, six IEEE reciprocals and lane broadcasts); the block form
+// with the translation block eliminated first.
+// Build: make -C tools solvebench        Run (GPU box): tools/solve_probe.sh
 #include "../slam-rgbd_amd/csrc/icp_kernels.hip"
 #include <cmath>
 #include <cstring>
 #include <vector>
 
+extern "C" int oracle_solve(const double* neq, double* xi);
+
 namespace {
 
-// The round-2 production solve (left-looking LDL^T, an early exit per pivot),
-// kept here verbatim as the bitwise reference for the right-looking form.
-__device__ __forceinline__ int solve_ref(const double* neq, double* T64, float* T32,
-                                                double* Lsh, int lane)
+__device__ __forceinline__ int tri6(int a, int b)  // upper-triangle index, a <= b
 {
-    if (!(neq[28] >= 6.0)) return YOUTH_STATUS_FEW_MATCHES;
-    const int i = lane < 6 ? lane : 5;
-    double maxd = 0.0;
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-        const double da = neq[tri6(a, a)];
-        if (da > maxd) maxd = da;
-    }
-    if (!(maxd > 0.0)) return YOUTH_STATUS_DEGENERATE;
-    const double eps = 1e-12 * maxd;
-    double Ar[6], Lr[6], D[6], Dinv[6];
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-        Ar[j] = neq[i <= j ? tri6(i, j) : tri6(j, i)];
-        Lr[j] = 0.0;
-    }
-    // LDL^T, column j: lane i computes A[i][j] - sum_m (L[i][m] L[j][m]) D[m]
-    // (lane j: the pivot d_j); L[i][j] = s / d_j below the diagonal
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-        double sj = Ar[j];
-#pragma unroll
-        for (int m = 0; m < j; ++m) sj -= (Lr[m] * readlane64(Lr[m], j)) * D[m];
-        const double d = readlane64(sj, j);
-        if (!(d > eps)) return YOUTH_STATUS_DEGENERATE;
-        D[j] = d;
-        Dinv[j] = 1.0 / d;  // one divide per pivot; every use multiplies
-        Lr[j] = lane > j ? sj * Dinv[j] : (lane == j ? 1.0 : 0.0);
-    }
-    // forward: y_i = (-b_i - sum_{m<i} L[i][m] y_m) / d_i
-    double y = -neq[21 + i];
-#pragma unroll
-    for (int m = 0; m < 6; ++m) {
-        const double ym = readlane64(y, m);
-        y = lane > m ? y - Lr[m] * ym : y;
-    }
-    double dinv = Dinv[0];
-#pragma unroll
-    for (int j = 1; j < 6; ++j) dinv = i == j ? Dinv[j] : dinv;
-    y = y * dinv;
-    // back: x_i = y_i - sum_{m>i} L[m][i] x_m, m decreasing (column i of L via LDS)
-    if (lane < 6) {
-#pragma unroll
-        for (int j = 0; j < 6; ++j) Lsh[lane * 6 + j] = Lr[j];
-    }
-    double x = y;
-#pragma unroll
-    for (int m = 5; m >= 0; --m) {
-        const double xm = readlane64(x, m);
-        const double Lmi = Lsh[m * 6 + i];
-        x = lane < m ? x - Lmi * xm : x;
-    }
-    double xi[6];
-#pragma unroll
-    for (int m = 0; m < 6; ++m) xi[m] = readlane64(x, m);
-
-    // T <- exp(xi^) T (se3_exp_left), one output entry per lane
-    const double wx = xi[0], wy = xi[1], wz = xi[2];
-    const double th2 = (wx * wx + wy * wy) + wz * wz;
-    double a, b, c;
-    if (th2 < 0x1p-7) {  // spec a10: Taylor in th2 (oracle_se3_exp: same fma chain)
-        const double x2 = th2;
-        a = fma(x2, fma(x2, fma(x2, fma(x2, fma(x2, -0x1.ae64567f544e4p-26, 0x1.71de3a556c734p-19),
-                                          -0x1.a01a01a01a01ap-13), 0x1.1111111111111p-7),
-                        -0x1.5555555555555p-3), 0x1.0000000000000p+0);
-        b = fma(x2, fma(x2, fma(x2, fma(x2, fma(x2, -0x1.1eed8eff8d898p-29, 0x1.27e4fb7789f5cp-22),
-                                          -0x1.a01a01a01a01ap-16), 0x1.6c16c16c16c17p-10),
-                        -0x1.5555555555555p-5), 0x1.0000000000000p-1);
-        c = fma(x2, fma(x2, fma(x2, fma(x2, fma(x2, -0x1.6124613a86d09p-33, 0x1.ae64567f544e4p-26),
-                                          -0x1.71de3a556c734p-19), 0x1.a01a01a01a01ap-13),
-                        -0x1.1111111111111p-7), 0x1.5555555555555p-3);
-    } else {
-        const double th = sqrt(th2);
-        double sn, co;
-        sincos(th, &sn, &co);
-        a = sn / th;
-        b = (1.0 - co) / th2;
-        c = (th - sn) / (th2 * th);
-    }
-    const double Km[3][3] = {{0.0, -wz, wy}, {wz, 0.0, -wx}, {-wy, wx, 0.0}};
-    const int l = lane < 12 ? lane : 11;
-    const int r = l >> 2, col = l & 3;
-    double Kr[3];  // row r of Km
-#pragma unroll
-    for (int k = 0; k < 3; ++k) Kr[k] = r == 0 ? Km[0][k] : (r == 1 ? Km[1][k] : Km[2][k]);
-    double Er[3], Vr[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const double K2 = (Kr[0] * Km[0][k] + Kr[1] * Km[1][k]) + Kr[2] * Km[2][k];
-        const double I = (r == k) ? 1.0 : 0.0;
-        Er[k] = (I + a * Kr[k]) + b * K2;
-        Vr[k] = (I + b * Kr[k]) + c * K2;
-    }
-    const double Er3 = (Vr[0] * xi[3] + Vr[1] * xi[4]) + Vr[2] * xi[5];
-    double o = (Er[0] * T64[0 * 4 + col] + Er[1] * T64[1 * 4 + col]) + Er[2] * T64[2 * 4 + col];
-    if (col == 3) o += Er3;
-    if (lane < 12) {
-        T64[lane] = o;
-        T32[lane] = (float)o;
-    }
-
-    return 0;
+    return a * 6 - (a * (a - 1)) / 2 + (b - a);
 }
 
-// Correctly rounded 1/d without the generic division's scaling and fixup:
-// v_rcp_f64, two Newton steps and a final FMA correction (Markstein), for
-// positive normal d away from the exponent ends and not of significand
-// 2 - 2^-52 (the known exception); anything else takes 1.0 / d.  d is
-// wave-uniform in the solve (a readlane), so the test is a scalar branch.
-__device__ __forceinline__ double rcp64_rn(double d)
-{
-    const unsigned long long bits = (unsigned long long)__double_as_longlong(d);
-    const unsigned ex = (unsigned)(bits >> 52);  // sign 0 for d > 0
-    const bool ok = ex >= 64u && ex <= 1983u && (bits & 0xFFFFFFFFFFFFFull) != 0xFFFFFFFFFFFFFull;
-    if (!ok) return 1.0 / d;
-    double r = __builtin_amdgcn_rcp(d);
-    double e = fma(-d, r, 1.0);
-    r = fma(r, e, r);
-    e = fma(-d, r, 1.0);
-    r = fma(r, e, r);
-    e = fma(-d, r, 1.0);
-    return fma(r, e, r);
-}
-
-__device__ __forceinline__ int solve_fast(const double* neq, double* T64, float* T32,
+__device__ __forceinline__ int solve_ldlt_wave(const double* neq, double* T64, float* T32,
                                                 double* Lsh, int lane)
 {
     if (!(neq[28] >= 6.0)) return YOUTH_STATUS_FEW_MATCHES;
@@ -172,7 +53,7 @@ __device__ __forceinline__ int solve_fast(const double* neq, double* T64, float*
         const double d = readlane64(S[m], m);
         bad |= !(d > eps);
         D[m] = d;
-        Dinv[m] = rcp64_rn(d);  // one divide per pivot; every use multiplies
+        Dinv[m] = 1.0 / d;  // one divide per pivot; every use multiplies
         Lr[m] = lane > m ? S[m] * Dinv[m] : (lane == m ? 1.0 : 0.0);
 #pragma unroll
         for (int j = m + 1; j < 6; ++j) S[j] -= (Lr[m] * readlane64(Lr[m], j)) * D[m];
@@ -248,6 +129,189 @@ __device__ __forceinline__ int solve_fast(const double* neq, double* T64, float*
 }
 
 
+
+// ---- the alternative block order (round 5 A/B): the translation block
+// eliminated first, upsilon = (u - M omega) / detG.  Fewer dependent steps
+// before exp's polynomials on paper, but slower here and 2-3x more sensitive
+// to the sums' last bits on ill-conditioned frames.
+__device__ __forceinline__ double dd2t(double a, double b, double c, double d)
+{
+    return fma(a, b, -(c * d));  // a b - c d
+}
+__device__ __forceinline__ double dot3t(double a0, double b0, double a1, double b1, double a2,
+                                       double b2)
+{
+    return fma(a2, b2, fma(a1, b1, a0 * b0));
+}
+// symmetric 3x3 {m00, m01, m02, m11, m12, m22}: adjugate, matrix-vector
+__device__ __forceinline__ void adj3t(const double* p, double* c)
+{
+    c[0] = dd2t(p[3], p[5], p[4], p[4]);
+    c[1] = dd2t(p[2], p[4], p[1], p[5]);
+    c[2] = dd2t(p[1], p[4], p[2], p[3]);
+    c[3] = dd2t(p[0], p[5], p[2], p[2]);
+    c[4] = dd2t(p[1], p[2], p[0], p[4]);
+    c[5] = dd2t(p[0], p[3], p[1], p[1]);
+}
+__device__ __forceinline__ void symv3t(const double* c, const double* v, double* o)
+{
+    o[0] = dot3t(c[0], v[0], c[1], v[1], c[2], v[2]);
+    o[1] = dot3t(c[1], v[0], c[3], v[1], c[4], v[2]);
+    o[2] = dot3t(c[2], v[0], c[4], v[1], c[5], v[2]);
+}
+// neq wave-uniform (LDS or registers); every lane computes everything, so no
+// value crosses lanes.  xi is zeroed on a nonzero status.
+__device__ __forceinline__ int solve_tfirst6(const double* neq, double xi[6])
+{
+#pragma unroll
+    for (int i = 0; i < 6; ++i) xi[i] = 0.0;
+    if (!(neq[28] >= 6.0)) return YOUTH_STATUS_FEW_MATCHES;
+    double maxd = 0.0;  // the diagonal, in order (a, a) = 0, 6, 11, 15, 18, 20
+    maxd = neq[0] > maxd ? neq[0] : maxd;
+    maxd = neq[6] > maxd ? neq[6] : maxd;
+    maxd = neq[11] > maxd ? neq[11] : maxd;
+    maxd = neq[15] > maxd ? neq[15] : maxd;
+    maxd = neq[18] > maxd ? neq[18] : maxd;
+    maxd = neq[20] > maxd ? neq[20] : maxd;
+    if (!(maxd > 0.0)) return YOUTH_STATUS_DEGENERATE;
+    const double eps = 1e-12 * maxd;
+    const double G[6] = {neq[15], neq[16], neq[17], neq[18], neq[19], neq[20]};
+    const double H[6] = {neq[0], neq[1], neq[2], neq[6], neq[7], neq[11]};
+    // K[i][j] = A[3+i][j] = A[j][3+i]
+    const double K[3][3] = {{neq[3], neq[8], neq[12]}, {neq[4], neq[9], neq[13]},
+                            {neq[5], neq[10], neq[14]}};
+    const double br[3] = {neq[21], neq[22], neq[23]}, bt[3] = {neq[24], neq[25], neq[26]};
+    double C[6], E[6], S[6], M[3][3], u[3], y[3], v[3];
+    adj3t(G, C);
+    const double detG = dot3t(G[0], C[0], G[1], C[1], G[2], C[2]);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {  // M = C K, column by column
+        const double k3[3] = {K[0][j], K[1][j], K[2][j]};
+        double o[3];
+        symv3t(C, k3, o);
+        M[0][j] = o[0];
+        M[1][j] = o[1];
+        M[2][j] = o[2];
+    }
+    symv3t(C, bt, u);
+    // S' upper triangle (i <= j): detG H[i][j] - (K^T M)[i][j]
+    S[0] = fma(detG, H[0], -dot3t(K[0][0], M[0][0], K[1][0], M[1][0], K[2][0], M[2][0]));
+    S[1] = fma(detG, H[1], -dot3t(K[0][0], M[0][1], K[1][0], M[1][1], K[2][0], M[2][1]));
+    S[2] = fma(detG, H[2], -dot3t(K[0][0], M[0][2], K[1][0], M[1][2], K[2][0], M[2][2]));
+    S[3] = fma(detG, H[3], -dot3t(K[0][1], M[0][1], K[1][1], M[1][1], K[2][1], M[2][1]));
+    S[4] = fma(detG, H[4], -dot3t(K[0][1], M[0][2], K[1][1], M[1][2], K[2][1], M[2][2]));
+    S[5] = fma(detG, H[5], -dot3t(K[0][2], M[0][2], K[1][2], M[1][2], K[2][2], M[2][2]));
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+        y[j] = fma(detG, br[j], -dot3t(K[0][j], u[0], K[1][j], u[1], K[2][j], u[2]));
+    adj3t(S, E);
+    const double detS = dot3t(S[0], E[0], S[1], E[1], S[2], E[2]);
+    const double epsG = eps * detG;
+    // pivots G00, C22/G00, detG/C22, S'00/detG, E22/(detG S'00), detS/(detG E22)
+    const bool ok = (G[0] > eps) & (C[5] > eps * G[0]) & (detG > eps * C[5]) & (S[0] > epsG) &
+                    (E[5] > epsG * S[0]) & (detS > epsG * E[5]);
+    if (!ok) return YOUTH_STATUS_DEGENERATE;
+    const double rS = 1.0 / detS, rG = 1.0 / detG;
+    symv3t(E, y, v);
+    double w[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) w[i] = v[i] * rS;  // omega
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        xi[i] = -w[i];
+        xi[3 + i] = -((u[i] - dot3t(M[i][0], w[0], M[i][1], w[1], M[i][2], w[2])) * rG);
+    }
+    return 0;
+}
+
+// the candidate as a wave: every lane solves (wave-uniform), exp as production
+__device__ __forceinline__ int solve_tfirst_wave(const double* neq, double* T64, float* T32, int lane)
+{
+    double xi[6];
+    const int st = solve_tfirst6(neq, xi);
+    if (st) return st;
+    const double wx = xi[0], wy = xi[1], wz = xi[2];
+    const double th2 = (wx * wx + wy * wy) + wz * wz;
+    double a, b, c;
+    if (th2 < 0x1p-7) {
+        const double x2 = th2;
+        a = fma(x2, fma(x2, fma(x2, fma(x2, fma(x2, -0x1.ae64567f544e4p-26, 0x1.71de3a556c734p-19),
+                                          -0x1.a01a01a01a01ap-13), 0x1.1111111111111p-7),
+                        -0x1.5555555555555p-3), 0x1.0000000000000p+0);
+        b = fma(x2, fma(x2, fma(x2, fma(x2, fma(x2, -0x1.1eed8eff8d898p-29, 0x1.27e4fb7789f5cp-22),
+                                          -0x1.a01a01a01a01ap-16), 0x1.6c16c16c16c17p-10),
+                        -0x1.5555555555555p-5), 0x1.0000000000000p-1);
+        c = fma(x2, fma(x2, fma(x2, fma(x2, fma(x2, -0x1.6124613a86d09p-33, 0x1.ae64567f544e4p-26),
+                                          -0x1.71de3a556c734p-19), 0x1.a01a01a01a01ap-13),
+                        -0x1.1111111111111p-7), 0x1.5555555555555p-3);
+    } else {
+        const double th = sqrt(th2);
+        double sn, co;
+        sincos(th, &sn, &co);
+        a = sn / th;
+        b = (1.0 - co) / th2;
+        c = (th - sn) / (th2 * th);
+    }
+    const double Km[3][3] = {{0.0, -wz, wy}, {wz, 0.0, -wx}, {-wy, wx, 0.0}};
+    const int l = lane < 12 ? lane : 11;
+    const int r = l >> 2, col = l & 3;
+    double Kr[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) Kr[k] = r == 0 ? Km[0][k] : (r == 1 ? Km[1][k] : Km[2][k]);
+    double Er[3], Vr[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double K2 = (Kr[0] * Km[0][k] + Kr[1] * Km[1][k]) + Kr[2] * Km[2][k];
+        const double I = (r == k) ? 1.0 : 0.0;
+        Er[k] = (I + a * Kr[k]) + b * K2;
+        Vr[k] = (I + b * Kr[k]) + c * K2;
+    }
+    const double Er3 = (Vr[0] * xi[3] + Vr[1] * xi[4]) + Vr[2] * xi[5];
+    double o = (Er[0] * T64[0 * 4 + col] + Er[1] * T64[1 * 4 + col]) + Er[2] * T64[2 * 4 + col];
+    if (col == 3) o += Er3;
+    if (lane < 12) {
+        T64[lane] = o;
+        T32[lane] = (float)o;
+    }
+    return 0;
+}
+
+// latency probes (one wave): dependent chains, s_memtime cycles per link
+__global__ void k_lat(double seed, int n, unsigned long long* out, double* sink)
+{
+    const int lane = threadIdx.x;
+    double x = seed + lane * 1e-9;
+    unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    for (int i = 0; i < n; ++i) x = fma(x, 0.999999, 1e-7);
+    unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    double y = seed + 1.0;
+    for (int i = 0; i < n; ++i) y = 1.0 / (y + 1.0);
+    unsigned long long t2 = __builtin_amdgcn_s_memtime();
+    double z = seed + 2.0;
+    for (int i = 0; i < n; ++i) z = readlane64(z * 1.0000001, i & 63);
+    unsigned long long t3 = __builtin_amdgcn_s_memtime();
+    double a0 = x, a1 = x + 1, a2 = x + 2, a3 = x + 3;
+    for (int i = 0; i < n; ++i) {
+        a0 = fma(a0, 0.999999, 1e-7);
+        a1 = fma(a1, 0.999999, 1e-7);
+        a2 = fma(a2, 0.999999, 1e-7);
+        a3 = fma(a3, 0.999999, 1e-7);
+    }
+    unsigned long long t4 = __builtin_amdgcn_s_memtime();
+    float f = (float)seed;
+    for (int i = 0; i < n; ++i) f = fmaf(f, 0.999999f, 1e-7f);
+    unsigned long long t5 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) {
+        out[0] = t1 - t0;
+        out[1] = t2 - t1;
+        out[2] = t3 - t2;
+        out[3] = t4 - t3;
+        out[4] = t5 - t4;
+    }
+    sink[lane] = x + y + z + a0 + a1 + a2 + a3 + f;
+}
+
+
 template <int kVar>
 __global__ void k_bench(const double* neq0, double* T64g, int reps, unsigned long long* ns)
 {
@@ -260,9 +324,9 @@ __global__ void k_bench(const double* neq0, double* T64g, int reps, unsigned lon
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     int st = 0;
     for (int r = 0; r < reps; ++r) {
-        st |= kVar == 0   ? solve_update_wave(neq, T64, T32, L, lane)
-              : kVar == 2 ? solve_fast(neq, T64, T32, L, lane)
-                          : solve_ref(neq, T64, T32, L, lane);
+        st |= kVar == 0   ? solve_update_wave(neq, T64, T32, lane)
+              : kVar == 1 ? solve_ldlt_wave(neq, T64, T32, L, lane)
+                          : solve_tfirst_wave(neq, T64, T32, lane);
         // feed the pose back into b so every solve depends on the previous one
         if (lane == 0) neq[21] = neq0[21] + T64[3] * 1e-3;
         __syncthreads();
@@ -273,52 +337,14 @@ __global__ void k_bench(const double* neq0, double* T64g, int reps, unsigned lon
     if (lane == 0) ns[1] = (unsigned long long)st;
 }
 
-
-// Bitwise: one wave per case; case c's system is sys[c][kNeq]; both solves
-// start from the same pose; mismatching poses or statuses are counted.
-template <int kMode>
-__global__ void k_cmp(const double* sys, int n, unsigned long long* bad)
+// device solve_block6 on n systems (one lane per system) for the oracle check
+__global__ void k_xi(const double* sys, int n, double* xi_out, int* st_out)
 {
-    __shared__ double neq[kNeq], Ta[12], Tb[12], L[36];
-    __shared__ float T32a[12], T32b[12];
-    const int lane = threadIdx.x;
-    for (int c = blockIdx.x; c < n; c += gridDim.x) {
-        if (lane < kNeq) neq[lane] = sys[(size_t)c * kNeq + lane];
-        if (lane < 12) {
-            Ta[lane] = Tb[lane] = (lane % 5) == 0 ? 1.0 : 0.0;
-            T32a[lane] = T32b[lane] = 0.0f;  // written only by an update
-        }
-        __syncthreads();
-        const int sa = solve_update_wave(neq, Ta, T32a, L, lane);
-        __syncthreads();
-        const int sb = kMode == 0 ? solve_ref(neq, Tb, T32b, L, lane) : solve_fast(neq, Tb, T32b, L, lane);
-        __syncthreads();
-        const bool diff = lane < 12 && (__double_as_longlong(Ta[lane]) != __double_as_longlong(Tb[lane]) ||
-                                        __float_as_uint(T32a[lane]) != __float_as_uint(T32b[lane]));
-        const unsigned long long any = __ballot(diff) != 0ull || sa != sb;
-        if (lane == 0 && any) atomicAdd(bad, 1ull);
-        if (lane == 0 && sa) atomicAdd(bad + 1, 1ull);
-        __syncthreads();
-    }
-}
-// rcp64_rn vs 1.0 / d bitwise over n SplitMix64 doubles: random significands
-// with exponents across the whole positive range, plus significands next to
-// all-ones and to 1 (the hard cases).
-__global__ void k_rcp_test(unsigned long long n, unsigned long long* bad)
-{
-    unsigned long long nb = 0;
-    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-    for (unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; i < n; i += stride) {
-        unsigned long long st = i * 0x9E3779B97F4A7C15ull + 0x1234567ull;
-        const unsigned long long r1 = sm64(st), r2 = sm64(st);
-        unsigned long long man = r1 & 0xFFFFFFFFFFFFFull;
-        if ((i & 7) == 1) man = 0xFFFFFFFFFFFFFull - (r2 & 0xFF);   // next to all ones
-        if ((i & 7) == 2) man = r2 & 0xFF;                          // next to 1.0
-        const unsigned long long ex = 1 + (r2 >> 20) % 2046;        // every normal exponent
-        const double d = __longlong_as_double((long long)((ex << 52) | man));
-        nb += __double_as_longlong(rcp64_rn(d)) != __double_as_longlong(1.0 / d);
-    }
-    if (nb) atomicAdd(bad, nb);
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n) return;
+    double xi[6];
+    st_out[c] = solve_block6(sys + (size_t)c * kNeq, xi);
+    for (int i = 0; i < 6; ++i) xi_out[(size_t)c * 6 + i] = xi[i];
 }
 }  // namespace
 
@@ -339,25 +365,41 @@ int main()
     (void)hipMalloc(&dns, 16);
     (void)hipMemcpy(dn, h, sizeof(h), hipMemcpyHostToDevice);
     const int reps = 2000;
+    const char* names[3] = {"block, rotation first (production)", "LDL^T right-looking (round 1-4)",
+                            "block, translation first"};
     double T[3][12];
-    for (int v = 0; v < 3; ++v) {
-        unsigned long long ns[2] = {0, 0};
-        for (int w = 0; w < 2; ++w) {
-            if (v == 0) hipLaunchKernelGGL(k_bench<0>, dim3(1), dim3(64), 0, 0, dn, dT, reps, dns);
-            else if (v == 1) hipLaunchKernelGGL(k_bench<1>, dim3(1), dim3(64), 0, 0, dn, dT, reps, dns);
-            else hipLaunchKernelGGL(k_bench<2>, dim3(1), dim3(64), 0, 0, dn, dT, reps, dns);
-            (void)hipMemcpy(ns, dns, 16, hipMemcpyDeviceToHost);
+    for (int round = 0; round < 3; ++round)
+        for (int v = 0; v < 3; ++v) {
+            unsigned long long ns[2] = {0, 0};
+            for (int w = 0; w < 2; ++w) {
+                if (v == 0) hipLaunchKernelGGL(k_bench<0>, dim3(1), dim3(64), 0, 0, dn, dT, reps, dns);
+                else if (v == 1) hipLaunchKernelGGL(k_bench<1>, dim3(1), dim3(64), 0, 0, dn, dT, reps, dns);
+                else hipLaunchKernelGGL(k_bench<2>, dim3(1), dim3(64), 0, 0, dn, dT, reps, dns);
+                (void)hipMemcpy(ns, dns, 16, hipMemcpyDeviceToHost);
+            }
+            (void)hipMemcpy(T[v], dT, sizeof(T[v]), hipMemcpyDeviceToHost);
+            printf("round %d  %-40s %7.0f ns per solve + update (one wave, %d dependent), status %llu\n",
+                   round, names[v], (double)ns[0] / reps, reps, ns[1]);
         }
-        (void)hipMemcpy(T[v], dT, sizeof(T[v]), hipMemcpyDeviceToHost);
-        printf("%-34s %7.0f ns per solve (one wave, %d dependent solves), status %llu\n",
-               v == 0 ? "solve_update_wave (right-looking)" : v == 1 ? "left-looking reference" : "right-looking, rcp64_rn pivots", (double)ns[0] / reps,
-               reps, ns[1]);
+    for (int v = 1; v < 3; ++v) {
+        double md = 0;
+        for (int q = 0; q < 12; ++q) md = fmax(md, fabs(T[v][q] - T[0][q]));
+        printf("pose after the chain, %s vs production: max |diff| %.3g\n", names[v], md);
     }
-    printf("pose after the chain: t = (%.17g, %.17g, %.17g), bitwise equal: %d %d\n", T[0][3], T[0][7],
-           T[0][11], memcmp(T[0], T[1], sizeof(T[0])) == 0, memcmp(T[0], T[2], sizeof(T[0])) == 0);
-
+    {
+        unsigned long long* dl;
+        double* dsink;
+        (void)hipMalloc(&dl, 64);
+        (void)hipMalloc(&dsink, 64 * 8);
+        for (int w = 0; w < 2; ++w) hipLaunchKernelGGL(k_lat, dim3(1), dim3(64), 0, 0, 0.5, 4096, dl, dsink);
+        unsigned long long l[5];
+        (void)hipMemcpy(l, dl, sizeof(l), hipMemcpyDeviceToHost);
+        printf("latency (s_memtime per link, one wave, 4096 links): fma_f64 dep %.2f, 1.0/x dep %.2f, "
+               "readlane64 dep %.2f, fma_f64 4 chains %.2f per fma, fma_f32 dep %.2f\n",
+               l[0] / 4096.0, l[1] / 4096.0, l[2] / 4096.0, l[3] / 4096.0 / 4, l[4] / 4096.0);
+    }
     // random systems: A = sum of r outer products of random 6-vectors (rank r
-    // = 1..8: rank < 6 is singular, its pivots fail), plus b, count, Sigma r^2
+    // = 1..8: rank < 6 is singular), b, count, Sigma r^2; device vs oracle
     {
         const int n = 1 << 18;
         std::vector<double> sys((size_t)n * kNeq);
@@ -374,36 +416,33 @@ int main()
                 if (r >= rank) for (int q = 0; q < 6; ++q) v[q] = 0.0;
                 for (int a = 0; a < 6; ++a) for (int b2 = 0; b2 < 6; ++b2) A[a][b2] += v[a] * v[b2];
             }
-            double* h = sys.data() + (size_t)c * kNeq;
-            int k = 0;
-            for (int a = 0; a < 6; ++a) for (int b2 = a; b2 < 6; ++b2) h[k++] = A[a][b2];
-            for (int q = 0; q < 6; ++q) h[21 + q] = rnd() * 1e-3 * scale * scale;
-            h[27] = 1.0;
-            h[28] = (c % 97 == 0) ? 3.0 : 1000.0;  // some too-few-matches cases
+            double* hh = sys.data() + (size_t)c * kNeq;
+            int kk = 0;
+            for (int a = 0; a < 6; ++a) for (int b2 = a; b2 < 6; ++b2) hh[kk++] = A[a][b2];
+            for (int q = 0; q < 6; ++q) hh[21 + q] = rnd() * 1e-3 * scale * scale;
+            hh[27] = 1.0;
+            hh[28] = (c % 97 == 0) ? 3.0 : 1000.0;  // some too-few-matches cases
         }
-        double* dsys;
+        double *dsys, *dxi;
+        int* dst;
         (void)hipMalloc(&dsys, sys.size() * sizeof(double));
+        (void)hipMalloc(&dxi, (size_t)n * 6 * 8);
+        (void)hipMalloc(&dst, (size_t)n * 4);
         (void)hipMemcpy(dsys, sys.data(), sys.size() * sizeof(double), hipMemcpyHostToDevice);
-        (void)hipMemset(dns, 0, 16);
-        for (int mode = 0; mode < 2; ++mode) {
-            (void)hipMemset(dns, 0, 16);
-            if (mode == 0) hipLaunchKernelGGL(k_cmp<0>, dim3(4096), dim3(64), 0, 0, dsys, n, dns);
-            else hipLaunchKernelGGL(k_cmp<1>, dim3(4096), dim3(64), 0, 0, dsys, n, dns);
-            unsigned long long b[2] = {0, 0};
-            (void)hipMemcpy(b, dns, 16, hipMemcpyDeviceToHost);
-            printf("right-looking vs %s: %llu mismatching cases of %d random systems "
-                   "(%llu with a nonzero status)\n", mode == 0 ? "left-looking solve" : "rcp64_rn pivots",
-                   b[0], n, b[1]);
+        hipLaunchKernelGGL(k_xi, dim3((n + 255) / 256), dim3(256), 0, 0, dsys, n, dxi, dst);
+        std::vector<double> gxi((size_t)n * 6);
+        std::vector<int> gst(n);
+        (void)hipMemcpy(gxi.data(), dxi, gxi.size() * 8, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(gst.data(), dst, gst.size() * 4, hipMemcpyDeviceToHost);
+        long bad = 0, nz = 0;
+        for (int c = 0; c < n; ++c) {
+            double xi[6];
+            const int s = oracle_solve(sys.data() + (size_t)c * kNeq, xi);
+            nz += s != 0;
+            bad += s != gst[c] || memcmp(xi, gxi.data() + (size_t)c * 6, sizeof(xi)) != 0;
         }
-        (void)hipFree(dsys);
-    }
-    {
-        const unsigned long long n = 1ull << 33;  // 8.6e9 reciprocals
-        (void)hipMemset(dns, 0, 16);
-        hipLaunchKernelGGL(k_rcp_test, dim3(16384), dim3(256), 0, 0, n, dns);
-        unsigned long long b = 0;
-        (void)hipMemcpy(&b, dns, 8, hipMemcpyDeviceToHost);
-        printf("rcp64_rn vs 1.0 / d: %llu mismatches of %llu\n", b, n);
+        printf("solve_block6 (device) vs oracle_solve: %ld mismatching xi or status of %d random systems "
+               "(%ld with a nonzero status)\n", bad, n, nz);
     }
     return 0;
 }
