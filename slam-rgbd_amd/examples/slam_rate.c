@@ -21,7 +21,8 @@
  * With YOUTH_SLAM_TRACE=<file> set, the module's event trace
  * (youth_slam_trace_enable) covers the backlogged passes and is written to
  * <file> as "t_seconds kind arg" lines (tools/slam_trace.py reads it beside a
- * rocprofv3 kernel trace).
+ * rocprofv3 kernel trace); the live frames' events go to <file>.live
+ * (tools/slam_trace.py --live).
  *
  * usage: slam_rate <n_frames> <passes> [width height]
  */
@@ -131,13 +132,40 @@ int main(int argc, char** argv)
     resetSlam();
     youth_slam_wait_idle(20000);
     const int nl = n < 60 ? n : 60;
+    double* lt0 = (double*)malloc((size_t)nl * 2 * sizeof(double));
+    if (!lt0) return 3;
+    if (trace_path && youth_slam_trace_enable(trace_cap) != 0) return 7;
     for (int k = 0; k < nl; ++k) {
         const double t0 = now_s();
         processSlamFrame(frames + (size_t)k * N, NULL, W, H, (uint32_t)k);
         while (youth_slam_trajectory_length() < k + 1) {
         }
-        lat[k] = (now_s() - t0) * 1e6;
+        const double t1 = now_s();
+        lat[k] = (t1 - t0) * 1e6;
+        lt0[2 * k] = t0;
+        lt0[2 * k + 1] = t1;
     }
+    if (trace_path) {
+        // the live frames' events: <file>.live, one "# live k t0 t1" line per frame
+        double* tt = (double*)malloc(trace_cap * sizeof(double));
+        int* tk = (int*)malloc(trace_cap * sizeof(int));
+        int* ta = (int*)malloc(trace_cap * sizeof(int));
+        if (!tt || !tk || !ta) return 3;
+        int ne = youth_slam_trace_read(trace_cap, tt, tk, ta);
+        if (ne > trace_cap) ne = trace_cap;
+        youth_slam_trace_enable(0);
+        char lp[4096];
+        snprintf(lp, sizeof(lp), "%s.live", trace_path);
+        FILE* f = fopen(lp, "w");
+        if (!f) return 8;
+        for (int k = 0; k < nl; ++k) fprintf(f, "# live %d %.9f %.9f\n", k, lt0[2 * k], lt0[2 * k + 1]);
+        for (int i = 0; i < ne; ++i) fprintf(f, "%.9f %d %d\n", tt[i], tk[i], ta[i]);
+        fclose(f);
+        free(tt);
+        free(tk);
+        free(ta);
+    }
+    free(lt0);
     stopSlamModule();
     double sorted[64];
     memcpy(sorted, rate, (size_t)passes * sizeof(double));

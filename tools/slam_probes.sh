@@ -14,6 +14,9 @@
 #               program (does any hipMemcpyAsync enqueue block > 1 ms?)
 #   library     tools/trk_stall_probe.py: the tracker driven from one thread
 #   runtime_log slam_rate with AMD_LOG_LEVEL=4 (the HIP runtime's own log)
+#   live        slam_rate under rocprofv3 --kernel-trace with the event trace:
+#               where a live frame's processSlamFrame -> pose time goes
+#               (tools/slam_trace.py --live)
 set -eo pipefail
 export TMPDIR=/tmp
 PROBE=${PROBE:-${1:-copy_paths}}
@@ -32,6 +35,14 @@ slam_rate_run() {  # label passes env...
 }
 
 case $PROBE in
+  live)
+    YOUTH_SLAM_TRACE=$O/events_live.txt timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv \
+        -d $O/kt_live -o kt -- slam-rgbd_amd/slam_rate 300 4 > $O/slam_rate_live.json 2> $O/slam_rate_live.err
+    KT=$(find $O/kt_live -name '*kernel_trace.csv' -print -quit)
+    python3 tools/slam_trace.py --live $O/events_live.txt.live $KT | tee $O/live_summary.txt
+    YOUTH_SLAM_TRACE=$O/events_live_noprof.txt timeout -k 10 120 slam-rgbd_amd/slam_rate 300 4 \
+        > $O/slam_rate_live_noprof.json 2> $O/slam_rate_live_noprof.err
+    python3 tools/slam_trace.py --live $O/events_live_noprof.txt.live | tee $O/live_summary_noprof.txt ;;
   copy_paths)
     slam_rate_run pull 20
     slam_rate_run sdma 20 YOUTH_ICP_TRACK_COPY=sdma

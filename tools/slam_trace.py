@@ -7,6 +7,10 @@ producer's push time, and the longest GPU-idle gap with the worker and
 producer events around it (which wait it sits in).
 
 usage: slam_trace.py TRACE [KERNEL_TRACE_CSV]
+       slam_trace.py --live TRACE.live [KERNEL_TRACE_CSV]
+(--live: slam_rate's one-frame-at-a-time phase, "# live k t0 t1" windows:
+the median time of each step of a frame from processSlamFrame's call to its
+pose in the trajectory, and the tracker kernels' span inside it)
 """
 import csv
 import sys
@@ -50,7 +54,56 @@ def spans(ev, begin, end):
     return out
 
 
+def live(path, kt=None):
+    wins, ev = [], []
+    with open(path) as f:
+        for ln in f:
+            if ln.startswith("# live"):
+                _, _, k, t0, t1 = ln.split()
+                wins.append((float(t0), float(t1)))
+            elif ln.strip():
+                t, k, a = ln.split()
+                ev.append((float(t), int(k), int(a)))
+    ks = kernels(kt) if kt else None
+    steps = {}
+
+    def add(name, v):
+        steps.setdefault(name, []).append(v * 1e6)
+    for t0, t1 in wins[1:]:              # the first frame starts the sequence
+        e = [x for x in ev if t0 <= x[0] <= t1]
+        first = {}
+        for t, k, a in e:
+            first.setdefault(k, t)
+        last = {}
+        for t, k, a in e:
+            last[k] = t
+        if not all(k in first for k in (2, 4, 5, 6, 7)):
+            continue
+        add("total", t1 - t0)
+        add("push (processSlamFrame copy)", first[2] - t0)
+        add("push end -> worker submit", first[4] - first[2])
+        add("submit (pull + launch enqueue)", first[5] - first[4])
+        add("submit end -> collect begin", first[6] - first[5])
+        add("collect (wait for the pose)", last[7] - first[6])
+        add("collect end -> pose seen", t1 - last[7])
+        if ks:
+            kk = [x for x in ks if first[4] - 1e-4 <= x[0] <= t1]
+            if kk:
+                add("first kernel start - submit begin", kk[0][0] - first[4])
+                add("kernels first start -> last end", max(x[1] for x in kk) - kk[0][0])
+                add("last kernel end -> collect end", last[7] - max(x[1] for x in kk))
+                for x in kk:
+                    add("kernel " + x[2].split("(")[0].replace("void ", ""), x[1] - x[0])
+    print(f"live frames: {len(wins) - 1} (median us per step)")
+    for k, v in steps.items():
+        v = sorted(v)
+        print(f"  {k:42s} {v[len(v) // 2]:8.1f}   (p10 {v[len(v) // 10]:7.1f}, p90 {v[(9 * len(v)) // 10]:7.1f})")
+
+
 def main():
+    if sys.argv[1] == "--live":
+        live(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)
+        return
     passes, ev = load(sys.argv[1])
     ks = kernels(sys.argv[2]) if len(sys.argv) > 2 else None
     for p, (t0, t1) in enumerate(passes):
