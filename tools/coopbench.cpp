@@ -139,7 +139,7 @@ int main(int argc, char** argv)
            "  entry->done %6.0f\n",
            median(pro[0]), median(pro[1]), median(pro[2]), median(pro[3]), median(pro[4]),
            median(pro[5]));
-    printf("  chunk-0 lane 0: column sums -> solve %6.0f   LDL^T solve %6.0f   SE(3) exp %6.0f\n",
+    printf("  chunk-0 lane 0: column sums -> solve %6.0f   solve + SE(3) update %6.0f   after %6.0f\n",
            median(sol[0]), median(sol[1]), median(sol[2]));
     youth_icp_destroy(c);
     return 0;

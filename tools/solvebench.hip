@@ -312,6 +312,124 @@ __global__ void k_lat(double seed, int n, unsigned long long* out, double* sink)
 }
 
 
+
+// ---- round-5 follow-up candidates (A/B only): the rotation-first block
+// solve with x1 = (u - M x2) / detP (u = C b1 and M = C Q are formed early,
+// so x1 is one dot product after x2 instead of two), and optionally the
+// exp's three degree-5 polynomials by Estrin (3 dependent fmas) instead of
+// Horner (5).
+template <bool kEstrin>
+__device__ __forceinline__ int solve_m_wave(const double* neq, double* T64, float* T32, int lane)
+{
+    double xi[6];
+    {
+        for (int i = 0; i < 6; ++i) xi[i] = 0.0;
+        if (!(neq[28] >= 6.0)) return YOUTH_STATUS_FEW_MATCHES;
+        double maxd = 0.0;
+        maxd = neq[0] > maxd ? neq[0] : maxd;
+        maxd = neq[6] > maxd ? neq[6] : maxd;
+        maxd = neq[11] > maxd ? neq[11] : maxd;
+        maxd = neq[15] > maxd ? neq[15] : maxd;
+        maxd = neq[18] > maxd ? neq[18] : maxd;
+        maxd = neq[20] > maxd ? neq[20] : maxd;
+        if (!(maxd > 0.0)) return YOUTH_STATUS_DEGENERATE;
+        const double eps = 1e-12 * maxd;
+        const double P[6] = {neq[0], neq[1], neq[2], neq[6], neq[7], neq[11]};
+        const double R[6] = {neq[15], neq[16], neq[17], neq[18], neq[19], neq[20]};
+        const double Q[3][3] = {{neq[3], neq[4], neq[5]}, {neq[8], neq[9], neq[10]},
+                                {neq[12], neq[13], neq[14]}};
+        const double b1[3] = {neq[21], neq[22], neq[23]}, b2[3] = {neq[24], neq[25], neq[26]};
+        double C[6], E[6], S[6], M[3][3], u[3], y[3], v[3], x2[3];
+        adj3(P, C);
+        const double detP = dot3(P[0], C[0], P[1], C[1], P[2], C[2]);
+        for (int j = 0; j < 3; ++j) {
+            const double q[3] = {Q[0][j], Q[1][j], Q[2][j]};
+            double o[3];
+            symv3(C, q, o);
+            M[0][j] = o[0];
+            M[1][j] = o[1];
+            M[2][j] = o[2];
+        }
+        symv3(C, b1, u);
+        S[0] = fma(detP, R[0], -dot3(Q[0][0], M[0][0], Q[1][0], M[1][0], Q[2][0], M[2][0]));
+        S[1] = fma(detP, R[1], -dot3(Q[0][0], M[0][1], Q[1][0], M[1][1], Q[2][0], M[2][1]));
+        S[2] = fma(detP, R[2], -dot3(Q[0][0], M[0][2], Q[1][0], M[1][2], Q[2][0], M[2][2]));
+        S[3] = fma(detP, R[3], -dot3(Q[0][1], M[0][1], Q[1][1], M[1][1], Q[2][1], M[2][1]));
+        S[4] = fma(detP, R[4], -dot3(Q[0][1], M[0][2], Q[1][1], M[1][2], Q[2][1], M[2][2]));
+        S[5] = fma(detP, R[5], -dot3(Q[0][2], M[0][2], Q[1][2], M[1][2], Q[2][2], M[2][2]));
+        for (int j = 0; j < 3; ++j)
+            y[j] = fma(detP, b2[j], -dot3(Q[0][j], u[0], Q[1][j], u[1], Q[2][j], u[2]));
+        adj3(S, E);
+        const double detS = dot3(S[0], E[0], S[1], E[1], S[2], E[2]);
+        const double epsP = eps * detP;
+        const bool ok = (P[0] > eps) & (C[5] > eps * P[0]) & (detP > eps * C[5]) & (S[0] > epsP) &
+                        (E[5] > epsP * S[0]) & (detS > epsP * E[5]);
+        if (!ok) return YOUTH_STATUS_DEGENERATE;
+        const double rS = 1.0 / detS, rP = 1.0 / detP;
+        symv3(E, y, v);
+        for (int i = 0; i < 3; ++i) x2[i] = v[i] * rS;
+        for (int i = 0; i < 3; ++i) {
+            xi[i] = -((u[i] - dot3(M[i][0], x2[0], M[i][1], x2[1], M[i][2], x2[2])) * rP);
+            xi[3 + i] = -x2[i];
+        }
+    }
+    const double wx = xi[0], wy = xi[1], wz = xi[2];
+    const double th2 = (wx * wx + wy * wy) + wz * wz;
+    double a, b, c;
+    if (th2 < 0x1p-7) {
+        const double x = th2;
+        if (kEstrin) {
+            const double x2 = x * x;
+            a = fma(fma(fma(x, -0x1.ae64567f544e4p-26, 0x1.71de3a556c734p-19), x2,
+                        fma(x, -0x1.a01a01a01a01ap-13, 0x1.1111111111111p-7)), x2,
+                    fma(x, -0x1.5555555555555p-3, 0x1.0000000000000p+0));
+            b = fma(fma(fma(x, -0x1.1eed8eff8d898p-29, 0x1.27e4fb7789f5cp-22), x2,
+                        fma(x, -0x1.a01a01a01a01ap-16, 0x1.6c16c16c16c17p-10)), x2,
+                    fma(x, -0x1.5555555555555p-5, 0x1.0000000000000p-1));
+            c = fma(fma(fma(x, -0x1.6124613a86d09p-33, 0x1.ae64567f544e4p-26), x2,
+                        fma(x, -0x1.71de3a556c734p-19, 0x1.a01a01a01a01ap-13)), x2,
+                    fma(x, -0x1.1111111111111p-7, 0x1.5555555555555p-3));
+        } else {
+            a = fma(x, fma(x, fma(x, fma(x, fma(x, -0x1.ae64567f544e4p-26, 0x1.71de3a556c734p-19),
+                                            -0x1.a01a01a01a01ap-13), 0x1.1111111111111p-7),
+                           -0x1.5555555555555p-3), 0x1.0000000000000p+0);
+            b = fma(x, fma(x, fma(x, fma(x, fma(x, -0x1.1eed8eff8d898p-29, 0x1.27e4fb7789f5cp-22),
+                                            -0x1.a01a01a01a01ap-16), 0x1.6c16c16c16c17p-10),
+                           -0x1.5555555555555p-5), 0x1.0000000000000p-1);
+            c = fma(x, fma(x, fma(x, fma(x, fma(x, -0x1.6124613a86d09p-33, 0x1.ae64567f544e4p-26),
+                                            -0x1.71de3a556c734p-19), 0x1.a01a01a01a01ap-13),
+                           -0x1.1111111111111p-7), 0x1.5555555555555p-3);
+        }
+    } else {
+        const double th = sqrt(th2);
+        double sn, co;
+        sincos(th, &sn, &co);
+        a = sn / th;
+        b = (1.0 - co) / th2;
+        c = (th - sn) / (th2 * th);
+    }
+    const double Km[3][3] = {{0.0, -wz, wy}, {wz, 0.0, -wx}, {-wy, wx, 0.0}};
+    const int l = lane < 12 ? lane : 11;
+    const int r = l >> 2, col = l & 3;
+    double Kr[3];
+    for (int k = 0; k < 3; ++k) Kr[k] = r == 0 ? Km[0][k] : (r == 1 ? Km[1][k] : Km[2][k]);
+    double Er[3], Vr[3];
+    for (int k = 0; k < 3; ++k) {
+        const double K2 = (Kr[0] * Km[0][k] + Kr[1] * Km[1][k]) + Kr[2] * Km[2][k];
+        const double I = (r == k) ? 1.0 : 0.0;
+        Er[k] = (I + a * Kr[k]) + b * K2;
+        Vr[k] = (I + b * Kr[k]) + c * K2;
+    }
+    const double Er3 = (Vr[0] * xi[3] + Vr[1] * xi[4]) + Vr[2] * xi[5];
+    double o = (Er[0] * T64[0 * 4 + col] + Er[1] * T64[1 * 4 + col]) + Er[2] * T64[2 * 4 + col];
+    if (col == 3) o += Er3;
+    if (lane < 12) {
+        T64[lane] = o;
+        T32[lane] = (float)o;
+    }
+    return 0;
+}
+
 template <int kVar>
 __global__ void k_bench(const double* neq0, double* T64g, int reps, unsigned long long* ns)
 {
@@ -326,6 +444,8 @@ __global__ void k_bench(const double* neq0, double* T64g, int reps, unsigned lon
     for (int r = 0; r < reps; ++r) {
         st |= kVar == 0   ? solve_update_wave(neq, T64, T32, lane)
               : kVar == 1 ? solve_ldlt_wave(neq, T64, T32, L, lane)
+              : kVar == 3 ? solve_m_wave<false>(neq, T64, T32, lane)
+              : kVar == 4 ? solve_m_wave<true>(neq, T64, T32, lane)
                           : solve_tfirst_wave(neq, T64, T32, lane);
         // feed the pose back into b so every solve depends on the previous one
         if (lane == 0) neq[21] = neq0[21] + T64[3] * 1e-3;
@@ -365,23 +485,25 @@ int main()
     (void)hipMalloc(&dns, 16);
     (void)hipMemcpy(dn, h, sizeof(h), hipMemcpyHostToDevice);
     const int reps = 2000;
-    const char* names[3] = {"block, rotation first (production)", "LDL^T right-looking (round 1-4)",
-                            "block, translation first"};
-    double T[3][12];
+    const char* names[5] = {"block, rotation first (production)", "LDL^T right-looking (round 1-4)",
+                            "block, translation first", "block, x1 from M", "block, x1 from M, Estrin exp"};
+    double T[5][12];
     for (int round = 0; round < 3; ++round)
-        for (int v = 0; v < 3; ++v) {
+        for (int v = 0; v < 5; ++v) {
             unsigned long long ns[2] = {0, 0};
             for (int w = 0; w < 2; ++w) {
                 if (v == 0) hipLaunchKernelGGL(k_bench<0>, dim3(1), dim3(64), 0, 0, dn, dT, reps, dns);
                 else if (v == 1) hipLaunchKernelGGL(k_bench<1>, dim3(1), dim3(64), 0, 0, dn, dT, reps, dns);
-                else hipLaunchKernelGGL(k_bench<2>, dim3(1), dim3(64), 0, 0, dn, dT, reps, dns);
+                else if (v == 2) hipLaunchKernelGGL(k_bench<2>, dim3(1), dim3(64), 0, 0, dn, dT, reps, dns);
+                else if (v == 3) hipLaunchKernelGGL(k_bench<3>, dim3(1), dim3(64), 0, 0, dn, dT, reps, dns);
+                else hipLaunchKernelGGL(k_bench<4>, dim3(1), dim3(64), 0, 0, dn, dT, reps, dns);
                 (void)hipMemcpy(ns, dns, 16, hipMemcpyDeviceToHost);
             }
             (void)hipMemcpy(T[v], dT, sizeof(T[v]), hipMemcpyDeviceToHost);
             printf("round %d  %-40s %7.0f ns per solve + update (one wave, %d dependent), status %llu\n",
                    round, names[v], (double)ns[0] / reps, reps, ns[1]);
         }
-    for (int v = 1; v < 3; ++v) {
+    for (int v = 1; v < 5; ++v) {
         double md = 0;
         for (int q = 0; q < 12; ++q) md = fmax(md, fabs(T[v][q] - T[0][q]));
         printf("pose after the chain, %s vs production: max |diff| %.3g\n", names[v], md);
