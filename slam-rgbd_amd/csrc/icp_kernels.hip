@@ -1918,9 +1918,12 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
             if (lane == 1) first = icp_dequeue_issue(is, myq);
             double sum = 0.0;
             if (lane < kPartStride) {
-                if (lane < kNeq)
+                if (lane < kNeq) {  // the waves' sums as a pairwise tree (2 dependent adds)
+                    double r[kRedThreads / 64];
 #pragma unroll
-                    for (int w = 0; w < kRedThreads / 64; ++w) sum += red[w][lane];
+                    for (int w = 0; w < kRedThreads / 64; ++w) r[w] = red[w][lane];
+                    sum = tree_sum<kRedThreads / 64>(r);
+                }
                 st_u64_sc1(partials + ((size_t)p * is.nblk + c) * kPartStride + lane,
                            (unsigned long long)__double_as_longlong(sum));
             }
@@ -2302,9 +2305,12 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
             // ---- publish this chunk's partial (sc1, drained), then arrive
             double sum = 0.0;
             if (lane < kPartStride) {
-                if (lane < kNeq)
+                if (lane < kNeq) {  // the waves' sums as a pairwise tree (3 dependent adds)
+                    double r[kThreads / 64];
 #pragma unroll
-                    for (int w = 0; w < kThreads / 64; ++w) sum += red[w][lane];
+                    for (int w = 0; w < kThreads / 64; ++w) r[w] = red[w][lane];
+                    sum = tree_sum<kThreads / 64>(r);
+                }
                 st_u64_sc1(part + (size_t)c * kPartStride + lane,
                            (unsigned long long)__double_as_longlong(sum));
             }
