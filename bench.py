@@ -993,23 +993,32 @@ def slam_api_rate(a, frames, rel_plan, passes=5):
         for f in range(min(n, 24)):                   # warm: context, plan, page-locked pool
             lib.processSlamFrame(ptrs[f], None, W, H, f)
         youth_icp.slam_wait_idle(20000)
-        rates, batched = [], []
+        rates, batched, push_us = [], [], []
+        push, qsize, tlen, clock = lib.processSlamFrame, lib.youth_slam_queue_size, \
+            lib.youth_slam_trajectory_length, time.perf_counter
         for _ in range(passes):
             youth_icp.resetSlam()
             youth_icp.slam_wait_idle(20000)
             b0 = youth_icp.slam_batched_frames()
-            t0 = time.perf_counter()
+            in_push = 0.0
+            t0 = clock()
             for f in range(n):
-                while lib.youth_slam_queue_size() >= 10:
+                while qsize() >= 10:
                     pass
-                lib.processSlamFrame(ptrs[f], None, W, H, f)
-            while lib.youth_slam_trajectory_length() < n:
+                tp = clock()
+                push(ptrs[f], None, W, H, f)
+                in_push += clock() - tp
+            while tlen() < n:
                 pass
-            rates.append(n / (time.perf_counter() - t0))
+            rates.append(n / (clock() - t0))
             batched.append(youth_icp.slam_batched_frames() - b0)
+            push_us.append(in_push * 1e6 / n)
         ts, T = youth_icp.slam_trajectory()
         out.update({"value": float(np.median(rates)), "unit": "frames/s",
                     "pass_values": rates, "batched_frames_per_pass": batched,
+                    # the producer's time inside processSlamFrame (its copy into a
+                    # page-locked queue buffer), per frame and pass
+                    "push_us_per_frame": push_us,
                     "frames_recorded": int(len(ts)), "timestamps_in_order":
                     bool(np.array_equal(ts, np.arange(n, dtype=np.uint32)))})
         if rel_plan is not None:
