@@ -1993,27 +1993,39 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
 //   * its source pixels (npx per lane) are loaded and back-projected ONCE
 //     into LDS; its record gathers hit the same lines every iteration
 //     (L1/L2-warm);
-//   * per iteration ONE hand-off: each workgroup publishes its partial
-//     (sc1 stores, drained) and adds to one of 8 arrival counters of its pair
-//     (shard = c & 7, one 128-B line each); every workgroup polls the 8
-//     shards, then sums ALL the pair's partials in the fixed column order of
-//     k_icp's last arriver and solves itself.  Identical inputs and code give
-//     every workgroup the identical fp64 pose, so no pose is handed off.
-// Partials are double-buffered by iteration parity: a workgroup writes
-// iteration k+2's row only after every workgroup of its pair published k+1,
-// i.e. finished reading k's rows.  Arrival counters count across iterations
-// (after iteration k shard s holds (k+1) x its workgroup count); this call's
-// counter set and timeout word were zeroed by the previous call, and this
-// call zeroes the next call's (stream order: the set a call uses is never
-// the one it clears).  Co-residency is guaranteed by the cooperative launch;
+//   * per iteration ONE hand-off, and no counter in it: each workgroup
+//     stores its partial row (sc1, 8-byte stores) over a row that holds the
+//     EMPTY pattern, and every workgroup loads ALL the pair's rows, loading
+//     again every 16-byte piece that still holds EMPTY, then sums them in the
+//     fixed column order of k_icp's last arriver and solves itself.
+//     Identical inputs and code give every workgroup the identical fp64
+//     pose, so no pose is handed off.  The wait is the data itself: one
+//     memory round trip after the last row lands, where an arrival counter
+//     costs three (store drain + atomic, counter poll, row loads; round 5:
+//     publish + arrive 1.04, poll 0.80, row loads 1.16 us per iteration).
+// EMPTY is a signalling NaN (high word kPartEmptyHi): fp64 arithmetic never
+// yields one (NaN results are quiet), so a row value can never look empty;
+// each value is one 8-byte store and is checked on its own, so no ordering
+// between a row's values is needed.  Rows are triple-buffered by iteration
+// (k % 3): once a workgroup has seen every row of iteration k, every
+// workgroup of the pair has read iteration k-1's rows (it read them before it
+// stored k), so it resets its OWN row of buffer (k+2) % 3 = (k-1) % 3 to
+// EMPTY, drains, and only then stores iteration k+1: whoever loads
+// iteration k+2's rows has seen that k+1 row first, so it sees EMPTY or the
+// k+2 value, never the k-1 one.  Across calls the rows alternate between two
+// arenas with the counter sets: a call resets the rows the previous call
+// used in the other arena (stream order: the arena a call uses is never the
+// one it resets).  Co-residency is guaranteed by the cooperative launch;
 // every spin is still bounded (timeout -> YOUTH_STATUS_TIMEOUT, no hang).
-constexpr int kCoopShards = 8;
-constexpr int kCoopShardStride = 32;  // words: one 128-B line per shard
+constexpr int kCoopShardStride = 32;  // words: one 128-B line per counter
 constexpr int kCoopMaxPx = 32;       // source pixels per lane (LDS: 3 x 32 KB)
-constexpr int kCoopMaxPairs = 16;     // counter words per set: 16 x 8 x 32
-// counter set layout (words): [pair][shard][32] arrivals | timeout word (one
-// line) | [pair][32] prep-done counters
-constexpr int kCoopErrWord = kCoopMaxPairs * kCoopShards * kCoopShardStride;
+constexpr int kCoopMaxPairs = 16;
+constexpr int kCoopBufs = 3;         // partial-row buffers per arena (iteration k % 3)
+constexpr unsigned kPartEmptyHi = 0x7FF7A5A5u;  // EMPTY = 0x7FF7A5A5'7FF7A5A5 (a signalling NaN)
+constexpr unsigned long long kPartEmpty = 0x7FF7A5A57FF7A5A5ull;
+// counter set layout (words): timeout word (one line) | [pair][32] prep-done
+// counters
+constexpr int kCoopErrWord = 0;
 constexpr int kCoopPrepWords = kCoopErrWord + kCoopShardStride;
 constexpr int kCoopSetWords = kCoopPrepWords + kCoopMaxPairs * kCoopShardStride;
 constexpr int kCoopTileH = 24;  // fused prep tiles: 64 x 24 pixels (one per workgroup of a 640x480 pair: 200 tiles, G = 200)
@@ -2028,7 +2040,7 @@ struct CoopState {
     int32_t* status;       // [pair]
     double* stats;         // [pair][iters][2]
     float* T_out;          // [pair][16] fp32 4x4, or null
-    unsigned* set;         // this call's counters [pair][shard * 32] + timeout word
+    unsigned* set;         // this call's counters: timeout word + prep counters
     unsigned* set_next;    // the next call's: zeroed here
     unsigned* head_err;    // k_icp's queue words: error/telemetry cleared for get_poses
     int iters, n_pairs, G, npx;  // G workgroups per pair, npx source pixels per lane
@@ -2054,6 +2066,13 @@ struct CoopState {
     int chain;
     int tgt_slot[kCoopMaxChain], prep_slot[kCoopMaxChain];
     double* res_pair[kCoopMaxChain];
+    // partial rows: this call's arena [kCoopBufs][part_cap][kPartStride]
+    // (row p G + c), every row EMPTY at launch; the other arena, whose first
+    // part_reset rows of every buffer (the previous call's) are reset here
+    double* part;
+    double* part_next;
+    int part_cap, part_reset;
+    int poll_delay;  // x 64 clocks before the first pass over the rows
 };
 
 // Phase timestamps for tools/coopbench only (never in the product build):
@@ -2081,6 +2100,87 @@ __device__ unsigned long long* coop_phase;
     do {                        \
     } while (0)
 #endif
+
+// sum_pair_rows for k_icp_coop's counter-free hand-off: the same loads, sums
+// and order, but every 16-byte piece that still holds EMPTY (its row not
+// stored yet) is loaded again until none does.  The sums are those of
+// sum_pair_rows over the same rows, bit for bit.  Every spin is bounded: a
+// thread that passes kCoopSpinMax polls, or finds the timeout word set, sets
+// it and `stop` comes back non-zero in every thread (the caller stops).
+template <int kBatch>
+__device__ __forceinline__ double sum_pair_rows_polled(__amdgpu_buffer_rsrc_t rpart, int nblk,
+                                                       double (*colsum)[kPartStride],
+                                                       unsigned* err, int* sh_stop, int delay,
+                                                       int& stop)
+{
+    // rows land about when this workgroup's own did: the first pass waits
+    // `delay` x 64 clocks so that it finds most of them (a pass over EMPTY
+    // rows is traffic every workgroup pays again)
+    int d = delay;
+    for (; d >= 8; d -= 8) __builtin_amdgcn_s_sleep(8);
+    for (; d > 0; --d) __builtin_amdgcn_s_sleep(1);
+    const int t = threadIdx.x;
+    const int j = t / kPieces, q = t - j * kPieces;
+    int mine = 0;
+    if (j < kSumCols) {
+        double s0 = 0.0, s1 = 0.0;
+        for (int bb = j; bb < nblk; bb += kBatch * kSumCols) {
+            u4v v[kBatch];
+#pragma unroll
+            for (int i = 0; i < kBatch; ++i) {
+                const int b = bb + i * kSumCols;
+                // aux 16 = sc1 (bypass this CU's L1: written by other CUs)
+                v[i] = b < nblk ? __builtin_bit_cast(
+                                      u4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                               rpart, (b * kPartStride + 2 * q) * 8, 0, 16))
+                                : u4v{0u, 0u, 0u, 0u};
+            }
+            unsigned spins = 0;
+            for (;;) {
+                bool miss = false;
+#pragma unroll
+                for (int i = 0; i < kBatch; ++i) {
+                    if (v[i].y == kPartEmptyHi || v[i].w == kPartEmptyHi) {  // pad rows are 0
+                        miss = true;
+                        v[i] = __builtin_bit_cast(
+                            u4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                     rpart, ((bb + i * kSumCols) * kPartStride + 2 * q) * 8, 0, 16));
+                    }
+                }
+                if (!miss) break;
+                if (++spins > kCoopSpinMax || ((spins & 63u) == 0u && ld_u32_sc1(err) != 0u)) {
+                    __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    mine = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            double a0[kBatch], a1[kBatch];
+#pragma unroll
+            for (int i = 0; i < kBatch; ++i) {
+                a0[i] = __hiloint2double((int)v[i].y, (int)v[i].x);
+                a1[i] = __hiloint2double((int)v[i].w, (int)v[i].z);
+            }
+            s0 += tree_sum<kBatch>(a0);
+            s1 += tree_sum<kBatch>(a1);
+        }
+        colsum[j][2 * q] = s0;
+        colsum[j][2 * q + 1] = s1;
+    }
+    // stop: sh_stop is 0 while the loop runs and is only ever set to 1 (every
+    // thread then leaves the loop), so no reset is needed
+    if (mine) *sh_stop = 1;
+    __syncthreads();
+    stop = __builtin_amdgcn_readfirstlane(*sh_stop);
+    double tsum = 0.0;
+    if (t < kNeq) {
+        double c[kSumCols];
+#pragma unroll
+        for (int jj = 0; jj < kSumCols; ++jj) c[jj] = colsum[jj][t];
+        tsum = tree_sum<kSumCols>(c);
+    }
+    return tsum;
+}
 
 // Spec a7-a9 for Q source pixels already back-projected (px = pixel slots
 // s0 .. s0+Q-1 of this lane in the LDS planes X/Y/Z [slot][256]): transform,
@@ -2147,7 +2247,6 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
     const int p = blockIdx.x / G;
     const int c = blockIdx.x - p * G;
     const int N = W * H;
-    unsigned* cnt = cs.set + (size_t)p * kCoopShards * kCoopShardStride;
     unsigned* err = cs.set + kCoopErrWord;
     unsigned* prep_cnt = cs.set + kCoopPrepWords + (size_t)p * kCoopShardStride;
     // the prep counter this pair waits on: its own (prep_wait), or in a
@@ -2166,6 +2265,17 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
             st_u32_sc1(cs.head_err + kQError, 0u);
             st_u32_sc1(cs.head_err + kQSpins, 0u);
             st_u32_sc1(cs.head_err + kQWaited, 0u);
+        }
+    }
+    // the previous call's partial rows (the other arena) back to EMPTY, for
+    // the next call; spread over the whole grid
+    if (cs.part_reset > 0) {
+        const unsigned per = (unsigned)cs.part_reset * kPartStride;  // doubles per buffer
+        const unsigned stride = gridDim.x * kThreads;
+        for (unsigned i = blockIdx.x * kThreads + threadIdx.x; i < kCoopBufs * per; i += stride) {
+            const unsigned b = i / per;
+            st_u64_sc1(cs.part_next + (size_t)b * cs.part_cap * kPartStride + (i - b * per),
+                       kPartEmpty);
         }
     }
     if (threadIdx.x < 12) {
@@ -2232,10 +2342,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
     const __amdgpu_buffer_rsrc_t rrec = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float4*>(recs + (size_t)tgt_frame * P), (short)0,
         (int)(P * sizeof(float4)), 0x00020000);
-    // shard s of this pair holds (k+1) x n_s after iteration k
-    const int my_shard = c & (kCoopShards - 1);
-    const unsigned n_s = lane < kCoopShards ? (unsigned)((G - lane + kCoopShards - 1) / kCoopShards)
-                                            : 0u;
+    const size_t buf_stride = (size_t)cs.part_cap * kPartStride;  // doubles per buffer
+    double* const part0 = cs.part + (size_t)p * G * kPartStride;  // pair p's rows, buffer 0
     int32_t st_acc = 0;
     bool timeout = false;
     COOP_MARK(1, 15);  // source pixels staged
@@ -2260,6 +2368,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
         __syncthreads();
         timeout = __builtin_amdgcn_readfirstlane(sh_stop) != 0;
     } else {
+        if (threadIdx.x == 0) sh_stop = 0;
         __syncthreads();
     }
 
@@ -2298,11 +2407,14 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
             if (!(lane & 1) && (lane >> 1) < kNeq) red[wave][lane >> 1] = tot;
         }
         __syncthreads();
-        double* part = partials + (size_t)(k & 1) * cs.n_pairs * G * kPartStride +
-                       (size_t)p * G * kPartStride;
+        double* part = part0 + (size_t)(k % kCoopBufs) * buf_stride;
         COOP_MARK(k, 2);
         if (wave == 0) {
-            // ---- publish this chunk's partial (sc1, drained), then arrive
+            // ---- store this chunk's partial row (sc1) over its EMPTY row.
+            // The drain first: this wave's reset of its row of buffer
+            // (k+1) % 3 (stored at iteration k-1) must be visible before any
+            // value of iteration k is (see the hand-off above)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             double sum = 0.0;
             if (lane < kPartStride) {
                 if (lane < kNeq) {  // the waves' sums as a pairwise tree (3 dependent adds)
@@ -2314,42 +2426,22 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
                 st_u64_sc1(part + (size_t)c * kPartStride + lane,
                            (unsigned long long)__double_as_longlong(sum));
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0)
-                __hip_atomic_fetch_add(cnt + my_shard * kCoopShardStride, 1u, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
             COOP_MARK(k, 3);
-            // ---- wait for every workgroup of the pair: lanes 0..7 poll a shard each
-            const unsigned want = (unsigned)(k + 1) * n_s;
-            unsigned spins = 0;
-            int stop = 0;
-            for (;;) {
-                const unsigned have =
-                    lane < kCoopShards ? ld_u32_sc1(cnt + lane * kCoopShardStride) : 0u;
-                const bool done = __ballot(lane < kCoopShards && have < want) == 0ull;
-                if (done) break;
-                __builtin_amdgcn_s_sleep(1);
-                if (++spins > kCoopSpinMax || ld_u32_sc1(err) != 0u) {
-                    if (lane == 0)
-                        __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    stop = 1;
-                    break;
-                }
-            }
-            if (lane == 0) sh_stop = stop;
             COOP_MARK(k, 4);
         }
-        __syncthreads();
         COOP_MARK(k, 5);
-        if (__builtin_amdgcn_readfirstlane(sh_stop)) {
+        // ---- every workgroup sums the pair's partials in the same fixed
+        // order, as soon as each row has landed (no counter, no barrier)
+        const __amdgpu_buffer_rsrc_t rpart = __builtin_amdgcn_make_buffer_rsrc(
+            part, (short)0, G * kPartStride * (int)sizeof(double), 0x00020000);
+        int stop = 0;
+        const double tsum = sum_pair_rows_polled<16>(rpart, G, colsum, err, &sh_stop,
+                                                      cs.poll_delay, stop);
+        COOP_MARK(k, 6);
+        if (stop) {
             timeout = true;
             break;
         }
-        // ---- every workgroup sums the pair's partials in the same fixed order
-        const __amdgpu_buffer_rsrc_t rpart = __builtin_amdgcn_make_buffer_rsrc(
-            part, (short)0, G * kPartStride * (int)sizeof(double), 0x00020000);
-        const double tsum = sum_pair_rows<16>(rpart, G, colsum);
-        COOP_MARK(k, 6);
         if (wave == 0) {
             if (lane < kNeq) sh_neq[lane] = tsum;
             if (c == 0 && cs.stats && lane == 0) {
@@ -2359,6 +2451,13 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
             COOP_MARK(k, 8);
             st_acc |= solve_update_wave(sh_neq, sh_T64, sh_T, lane);
             COOP_MARK(k, 9);
+            // every row of iteration k seen: every workgroup of the pair has
+            // read iteration k-1's, so this row of that buffer ((k+2) % 3,
+            // written next at iteration k+2) goes back to EMPTY now
+            if (k + 2 < cs.iters && lane < kPartStride)
+                st_u64_sc1(part0 + (size_t)((k + 2) % kCoopBufs) * buf_stride +
+                               (size_t)c * kPartStride + lane,
+                           kPartEmpty);
             COOP_MARK(k, 10);
         }
         __syncthreads();
@@ -2551,7 +2650,11 @@ struct youth_icp_ctx {
     int coop_bpc_tall[2 * kVariants] = {};  // the 64 x 80 prep-tile kernel at 10 px per lane
     unsigned* d_coop = nullptr;      // 2 counter sets of kCoopSetWords
     int32_t* d_status_out = nullptr; // [max_frames] host batch API: status per pair of the call
-    int coop_par = 0;                // set used by the next coop call
+    int coop_par = 0;                // set (and partial-row arena) used by the next coop call
+    double* d_coop_part = nullptr;   // 2 arenas x kCoopBufs x coop_part_cap rows (EMPTY when idle)
+    int coop_part_cap = 0;           // rows per buffer
+    int coop_part_rows[2] = {0, 0};  // rows per buffer the last call on each arena used
+    int coop_poll_delay = -1;        // YOUTH_ICP_COOP_POLL_DELAY (x 64 clocks); -1: G / 8
     int last_coop_G = 0, last_coop_px = 0;
     bool last_coop = false;          // the last align ran k_icp_coop
 
@@ -2633,6 +2736,26 @@ static int reduce_geometry(const youth_icp_ctx* c, int n_pairs, int* chunk_out)
     nb = (c->N + chunk - 1) / chunk;
     *chunk_out = chunk;
     return nb;
+}
+
+// k_icp_coop's partial-row arenas, every row EMPTY (k_icp_coop comment).  A
+// call needing more rows than there are reallocates; the free and the fill
+// wait for the device, so no launch of this context still uses the old rows.
+static int ensure_coop_part(youth_icp_ctx* c, int rows)
+{
+    if (rows <= c->coop_part_cap) return YOUTH_OK;
+    const int cap = std::max(rows, c->n_cu * 2);
+    if (c->d_coop_part) HIP_TRY(hipFree(c->d_coop_part));
+    c->d_coop_part = nullptr;
+    c->coop_part_cap = 0;
+    const size_t doubles = (size_t)2 * kCoopBufs * cap * kPartStride;
+    HIP_TRY(hipMalloc(&c->d_coop_part, doubles * sizeof(double)));
+    static_assert((unsigned)(kPartEmpty >> 32) == (unsigned)kPartEmpty, "EMPTY fills by words");
+    HIP_TRY(hipMemsetD32((hipDeviceptr_t)c->d_coop_part, (int)kPartEmptyHi, doubles * 2));
+    HIP_TRY(hipDeviceSynchronize());
+    c->coop_part_cap = cap;
+    c->coop_part_rows[0] = c->coop_part_rows[1] = 0;
+    return YOUTH_OK;
 }
 
 static int ensure_partials(youth_icp_ctx* c, size_t doubles)
@@ -2969,10 +3092,11 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
                        const PrepJob* job)
 {
     const int iters = c->prm.iters;
-    int rc = ensure_partials(c, (size_t)2 * n_pairs * G * kPartStride);
+    int rc = ensure_coop_part(c, n_pairs * G);
     if (rc) return rc;
-    unsigned* set = c->d_coop + (size_t)c->coop_par * kCoopSetWords;
-    unsigned* set_next = c->d_coop + (size_t)(c->coop_par ^ 1) * kCoopSetWords;
+    const int par = c->coop_par;
+    unsigned* set = c->d_coop + (size_t)par * kCoopSetWords;
+    unsigned* set_next = c->d_coop + (size_t)(par ^ 1) * kCoopSetWords;
     c->coop_par ^= 1;
     const bool wide = job && (c->W % 4 == 0) && (reinterpret_cast<uintptr_t>(job->depth) % 8 == 0);
     // tile-shaped source chunks when one target tile is exactly one
@@ -3000,6 +3124,17 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
             cs.res_pair[i] = job->res[i];
         }
     }
+    const size_t arena = (size_t)kCoopBufs * c->coop_part_cap * kPartStride;
+    cs.part = c->d_coop_part + (size_t)par * arena;
+    cs.part_next = c->d_coop_part + (size_t)(par ^ 1) * arena;
+    cs.part_cap = c->coop_part_cap;
+    cs.part_reset = c->coop_part_rows[par ^ 1];  // the previous call's rows
+    // the first pass over the rows waits G / 8 x 64 clocks by default: the
+    // rows' landing spread grows with the rows every workgroup loads
+    // (profiles/r05/delay_sweep_r5s.txt, _r5t.txt: 640x480 (G 200) best at
+    // 20-24, 1280x960 (G 240) at 28-32; no wait 13.7 K / 4.93 K aligns/s,
+    // 24: 15.7 K / 5.32 K, 32: 15.3 K / 5.41 K; the tracker within noise)
+    cs.poll_delay = c->coop_poll_delay >= 0 ? c->coop_poll_delay : G / 8;
     const float4* recs = c->d_rec;
     size_t P = c->P;
     int W = c->W, H = c->H;
@@ -3013,7 +3148,12 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
     rc = ev_begin(c, s, &ep, 0);
     if (rc) return rc;
     rc = coop_enqueue(c, s, args, n_pairs * G, npx, tall);
-    if (rc) return rc;
+    if (rc) {
+        c->coop_par = par;  // nothing ran: the sets and arenas stay as they were
+        return rc;
+    }
+    c->coop_part_rows[par ^ 1] = 0;          // reset by this launch
+    c->coop_part_rows[par] = n_pairs * G;    // dirtied by it
     c->last_coop_G = G;
     c->last_coop_px = npx;
     c->lanes = youth_lanes{tile_src ? YOUTH_LANES_COOP_TILE : YOUTH_LANES_COOP, npx * c->coop_threads,
@@ -3337,7 +3477,7 @@ void youth_icp_destroy(youth_icp_ctx* c)
     void* bufs[] = {c->d_depth, c->d_rec,   c->d_xyz,      c->d_T64, c->d_T32,   c->d_status,
                     c->d_Tinit, c->d_stats, c->d_partials, c->d_neq, c->d_assoc, c->d_Tout,
                     c->d_flag,  c->d_arrivals, c->d_arr_it, c->d_epoch, c->d_head,
-                    c->d_coop,  c->d_status_out};
+                    c->d_coop,  c->d_status_out, c->d_coop_part};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->device >= 0 && c->device < 64) {
@@ -3458,6 +3598,8 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         }
         const char* nc = getenv("YOUTH_ICP_NO_COOP");
         c->coop = !(nc && *nc && *nc != '0');
+        const char* cpd = getenv("YOUTH_ICP_COOP_POLL_DELAY");  // tuning knob
+        if (cpd && atoi(cpd) >= 0) c->coop_poll_delay = atoi(cpd);
         const char* cpx = getenv("YOUTH_ICP_COOP_PX");
         if (cpx && atoi(cpx) >= 1 && atoi(cpx) <= kCoopMaxPx) c->coop_px = atoi(cpx);
         c->coop_px_env = c->coop_px;

@@ -1466,3 +1466,36 @@ def test_track_submit_pinned_pageable_buffers_fall_back():
                 for b in bufs:
                     b.close()
     assert np.array_equal(out[0], out[1])
+
+
+@pytest.mark.parametrize("iters", [1, 2, 3, 10])
+def test_coop_partial_rows_reused_across_call_sizes(iters):
+    """k_icp_coop's counter-free hand-off: every partial row is EMPTY before
+    it is stored, rows are triple-buffered by iteration and alternate between
+    two arenas by call, each call resetting the rows the previous one used.
+    Calls of 1, 8, 3 and 5 pairs (grids of different rows per buffer), in an
+    interleaved order on ONE context, with 1-3 iterations (the reset of buffer
+    (k+2) % 3 skipped or not) and 10: every result bit-identical to the same
+    call on a fresh context, no timeout, and the 1-pair pose within the bar
+    of the oracle."""
+    import torch
+    N = 640 * 480
+    src, dst, _ = youth_synth.pairs(52, 8)
+    ds, dd = torch.from_numpy(src).cuda(), torch.from_numpy(dst).cuda()
+    sizes = (1, 8, 3, 5)
+    want = {}
+    for n in sizes:
+        with youth_icp.IcpContext(640, 480, 16, iters=iters) as ctx:
+            ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), n)
+            assert ctx.get_plan()["kernel"] == "k_icp_coop"
+            T64, _, st = ctx.get_poses(n)
+            assert not st.any()
+            want[n] = T64.copy()
+    with youth_icp.IcpContext(640, 480, 16, iters=iters) as ctx:
+        for n in (8, 1, 5, 1, 3, 8, 3, 1, 5, 5, 8, 1):
+            ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), n)
+            T64, _, st = ctx.get_poses(n)
+            assert not st.any(), (n, st)
+            assert np.array_equal(T64, want[n]), n
+    To, _, sto, _ = oracle.align(src[0], dst[0], iters=iters)
+    assert sto == 0 and _pose_err(want[1][0], To) <= POSE_TOL

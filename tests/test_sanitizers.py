@@ -7,6 +7,7 @@ entry points the worker calls come from tests/tsan/icp_stub.c (a CPU
 stand-in linked only into this driver), so it runs without a GPU.  Host code
 only: GPU sanitizers are not available on the GPU pool.
 """
+import fcntl
 import os
 import subprocess
 
@@ -18,7 +19,10 @@ TSAN = os.path.join(HERE, "tsan")
 
 @pytest.fixture(scope="module")
 def drivers():
-    r = subprocess.run(["make", "-C", TSAN, "-j2"], capture_output=True, text=True)
+    # one build at a time (pytest-xdist workers share the object directories)
+    with open(os.path.join(TSAN, ".build.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        r = subprocess.run(["make", "-C", TSAN, "-j2"], capture_output=True, text=True)
     if r.returncode != 0:
         pytest.fail("sanitizer build failed:\n" + r.stdout + r.stderr)
     return TSAN

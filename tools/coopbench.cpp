@@ -5,9 +5,9 @@
 // Includes the production translation unit with YOUTH_COOP_PHASES, so thread
 // 0 of every workgroup stamps s_memrealtime (100 MHz) at 8 points of every
 // iteration: 0 start, 1 pixel loop done, 2 workgroup reduction done,
-// 3 partial published + arrival issued, 4 all arrivals seen, 5 barrier,
-// 6 partials summed, 7 solved.  Prints per-phase medians over workgroups and
-// iterations 1..iters-1, and the hand-off latency (last arrival -> first
+// 3 partial row stored, 4 = 3 and 5 = 4 (no counter, no barrier since the
+// counter-free hand-off), 6 every row seen and summed, 7 solved.  Prints per-phase medians over workgroups and
+// iterations 1..iters-1, and the hand-off latency (last row stored -> first
 // workgroup that saw them all).
 #define YOUTH_COOP_PHASES 1
 #include "../slam-rgbd_amd/csrc/icp_kernels.hip"
@@ -88,7 +88,7 @@ int main(int argc, char** argv)
                     for (int s = 0; s < 7; ++s) ph[s].push_back((at(b, k, s + 1) - at(b, k, s)) * 10.0);
                     if (k + 1 < iters) ph[7].push_back((at(b, k + 1, 0) - at(b, k, 7)) * 10.0);
                     last3 = std::max(last3, at(b, k, 3));
-                    first4 = std::min(first4, at(b, k, 4));
+                    first4 = std::min(first4, at(b, k, 6));  // last row stored -> first workgroup that summed them all
                     mn0 = std::min(mn0, at(b, k, 0));
                     mx0 = std::max(mx0, at(b, k, 0));
                 }
@@ -119,8 +119,8 @@ int main(int argc, char** argv)
             pro[5].push_back((at(b, iters - 1, 7) - t0) * 10.0);     // first entry -> last solve
         }
     }
-    const char* names[8] = {"pixel loop", "wg reduction", "publish+arrive", "poll (all arrived)",
-                            "barrier", "sum partials", "solve+barrier", "loop back"};
+    const char* names[8] = {"pixel loop", "wg reduction", "publish", "(no counter poll)",
+                            "(no barrier)", "poll rows + sum", "solve+barrier", "loop back"};
     printf("%dx%d pairs %d  G %d  px/lane %d  (ns, medians over workgroups x iterations 1..%d x %d reps)\n",
            W, H, n, G, npx, iters - 1, reps);
     double acc = 0;
