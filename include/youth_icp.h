@@ -55,7 +55,7 @@ typedef struct youth_icp_params {
 #define YOUTH_STATUS_OK          0
 #define YOUTH_STATUS_DEGENERATE  1 /* an iteration's 6x6 system was singular: update skipped */
 #define YOUTH_STATUS_FEW_MATCHES 2 /* an iteration had < 6 correspondences: update skipped */
-#define YOUTH_STATUS_TIMEOUT     4 /* the persistent align kernel hit its spin bound (never expected) */
+#define YOUTH_STATUS_TIMEOUT     4 /* an align kernel hit its spin bound (never expected) */
 
 /* Return codes of the additive API. */
 #define YOUTH_OK        0

@@ -2073,6 +2073,8 @@ struct CoopState {
     double* part_next;
     int part_cap, part_reset;
     int poll_delay;  // x 64 clocks before the first pass over the rows
+    unsigned spin_max;  // polls before a wait gives up (kCoopSpinMax; the test hook's less)
+    int stall_chunk;    // test hook: this chunk of pair 0 never stores iteration 1's row (-1: none)
 };
 
 // Phase timestamps for tools/coopbench only (never in the product build):
@@ -2105,13 +2107,13 @@ __device__ unsigned long long* coop_phase;
 // and order, but every 16-byte piece that still holds EMPTY (its row not
 // stored yet) is loaded again until none does.  The sums are those of
 // sum_pair_rows over the same rows, bit for bit.  Every spin is bounded: a
-// thread that passes kCoopSpinMax polls, or finds the timeout word set, sets
+// thread that passes spin_max polls, or finds the timeout word set, sets
 // it and `stop` comes back non-zero in every thread (the caller stops).
 template <int kBatch>
 __device__ __forceinline__ double sum_pair_rows_polled(__amdgpu_buffer_rsrc_t rpart, int nblk,
                                                        double (*colsum)[kPartStride],
                                                        unsigned* err, int* sh_stop, int delay,
-                                                       int& stop)
+                                                       unsigned spin_max, int& stop)
 {
     // rows land about when this workgroup's own did: the first pass waits
     // `delay` x 64 clocks so that it finds most of them (a pass over EMPTY
@@ -2148,7 +2150,7 @@ __device__ __forceinline__ double sum_pair_rows_polled(__amdgpu_buffer_rsrc_t rp
                     }
                 }
                 if (!miss) break;
-                if (++spins > kCoopSpinMax || ((spins & 63u) == 0u && ld_u32_sc1(err) != 0u)) {
+                if (++spins > spin_max || ((spins & 63u) == 0u && ld_u32_sc1(err) != 0u)) {
                     __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     mine = 1;
                     break;
@@ -2355,7 +2357,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
             int stop = 0;
             while (ld_u32_sc1(wait_cnt) < (unsigned)G) {
                 __builtin_amdgcn_s_sleep(1);
-                if (++spins > kCoopSpinMax || ld_u32_sc1(err) != 0u) {
+                if (++spins > cs.spin_max || ld_u32_sc1(err) != 0u) {
                     __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     stop = 1;
                     break;
@@ -2416,7 +2418,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
             // value of iteration k is (see the hand-off above)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             double sum = 0.0;
-            if (lane < kPartStride) {
+            if (lane < kPartStride && !(k == 1 && p == 0 && c == cs.stall_chunk)) {
                 if (lane < kNeq) {  // the waves' sums as a pairwise tree (3 dependent adds)
                     double r[kThreads / 64];
 #pragma unroll
@@ -2436,7 +2438,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
             part, (short)0, G * kPartStride * (int)sizeof(double), 0x00020000);
         int stop = 0;
         const double tsum = sum_pair_rows_polled<16>(rpart, G, colsum, err, &sh_stop,
-                                                      cs.poll_delay, stop);
+                                                      cs.poll_delay, cs.spin_max, stop);
         COOP_MARK(k, 6);
         if (stop) {
             timeout = true;
@@ -2655,6 +2657,7 @@ struct youth_icp_ctx {
     int coop_part_cap = 0;           // rows per buffer
     int coop_part_rows[2] = {0, 0};  // rows per buffer the last call on each arena used
     int coop_poll_delay = -1;        // YOUTH_ICP_COOP_POLL_DELAY (x 64 clocks); -1: G / 8
+    int coop_stall_once = -1;        // YOUTH_ICP_TEST_COOP_STALL (test hook, first coop launch only)
     int last_coop_G = 0, last_coop_px = 0;
     bool last_coop = false;          // the last align ran k_icp_coop
 
@@ -3135,6 +3138,11 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
     // 20-24, 1280x960 (G 240) at 28-32; no wait 13.7 K / 4.93 K aligns/s,
     // 24: 15.7 K / 5.32 K, 32: 15.3 K / 5.41 K; the tracker within noise)
     cs.poll_delay = c->coop_poll_delay >= 0 ? c->coop_poll_delay : G / 8;
+    // test hook (YOUTH_ICP_TEST_COOP_STALL=<chunk>): the context's first coop
+    // launch loses one row, so every wait times out after ~20 ms
+    cs.stall_chunk = c->coop_stall_once;
+    cs.spin_max = c->coop_stall_once >= 0 ? 20000u : kCoopSpinMax;
+    c->coop_stall_once = -1;
     const float4* recs = c->d_rec;
     size_t P = c->P;
     int W = c->W, H = c->H;
@@ -3619,6 +3627,8 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         // test hook (tests/test_gpu_parity.py): every cooperative launch of
         // this context is refused as the runtime would, exercising the
         // persistent fallback of run_iterations
+        const char* cst = getenv("YOUTH_ICP_TEST_COOP_STALL");
+        if (cst && atoi(cst) >= 0) c->coop_stall_once = atoi(cst);
         const char* crf = getenv("YOUTH_ICP_TEST_REFUSE_COOP");
         c->coop_refuse = crf && *crf && *crf != '0';
         const char* nqs = getenv("YOUTH_ICP_QUEUES");

@@ -41,6 +41,7 @@ REDUCE_LANE32 = 1  # YOUTH_REDUCE_LANE32 (opt-in): fp32 lane sums -> fp64, launc
 LANES_STRIDED, LANES_COOP, LANES_COOP_TILE = 0, 1, 2   # youth_lanes.kind
 STATUS_DEGENERATE = 1
 STATUS_FEW_MATCHES = 2
+STATUS_TIMEOUT = 4  # a kernel hit its spin bound (youth_icp.h YOUTH_STATUS_TIMEOUT)
 
 
 class IcpError(RuntimeError):

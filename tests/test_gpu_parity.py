@@ -1499,3 +1499,32 @@ def test_coop_partial_rows_reused_across_call_sizes(iters):
             assert np.array_equal(T64, want[n]), n
     To, _, sto, _ = oracle.align(src[0], dst[0], iters=iters)
     assert sto == 0 and _pose_err(want[1][0], To) <= POSE_TOL
+
+
+def test_coop_lost_row_times_out_and_context_recovers(monkeypatch):
+    """A k_icp_coop launch in which one workgroup never stores its partial
+    row (test hook YOUTH_ICP_TEST_COOP_STALL: chunk 7 of pair 0 skips
+    iteration 1's row; the hook's waits give up after 20000 polls) ends with
+    YOUTH_STATUS_TIMEOUT instead of hanging, and leaves its arena part EMPTY
+    and part written: the same context's next calls (on the other arena,
+    then on the reset one) give every pose bit-identical to a fresh
+    context's."""
+    import torch
+    src, dst, _ = youth_synth.pairs(53, 3)
+    ds, dd = torch.from_numpy(src).cuda(), torch.from_numpy(dst).cuda()
+    want = {}
+    for n in (1, 3):
+        with youth_icp.IcpContext(640, 480, 4) as ctx:
+            ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), n)
+            want[n] = ctx.get_poses(n)[0].copy()
+    monkeypatch.setenv("YOUTH_ICP_TEST_COOP_STALL", "7")
+    with youth_icp.IcpContext(640, 480, 4) as ctx:
+        ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), 1)
+        assert ctx.get_plan()["kernel"] == "k_icp_coop"
+        st = ctx.get_poses(1)[2]
+        assert st[0] & youth_icp.STATUS_TIMEOUT, st
+        for n in (3, 1, 3):
+            ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), n)
+            T64, _, st = ctx.get_poses(n)
+            assert not st.any(), (n, st)
+            assert np.array_equal(T64, want[n]), n
