@@ -2742,9 +2742,11 @@ static int reduce_geometry(const youth_icp_ctx* c, int n_pairs, int* chunk_out)
 }
 
 // k_icp_coop's partial-row arenas, every row EMPTY (k_icp_coop comment).  A
-// call needing more rows than there are reallocates; the free and the fill
-// wait for the device, so no launch of this context still uses the old rows.
-static int ensure_coop_part(youth_icp_ctx* c, int rows)
+// call needing more rows than there are reallocates (hipFree waits for the
+// device, so no launch still uses the old rows).  The EMPTY fill is enqueued
+// on the launch's stream ahead of the launch; any later coop launch of this
+// context is ordered after this one (coop_enqueue), so after the fill too.
+static int ensure_coop_part(youth_icp_ctx* c, hipStream_t s, int rows)
 {
     if (rows <= c->coop_part_cap) return YOUTH_OK;
     const int cap = std::max(rows, c->n_cu * 2);
@@ -2754,8 +2756,7 @@ static int ensure_coop_part(youth_icp_ctx* c, int rows)
     const size_t doubles = (size_t)2 * kCoopBufs * cap * kPartStride;
     HIP_TRY(hipMalloc(&c->d_coop_part, doubles * sizeof(double)));
     static_assert((unsigned)(kPartEmpty >> 32) == (unsigned)kPartEmpty, "EMPTY fills by words");
-    HIP_TRY(hipMemsetD32((hipDeviceptr_t)c->d_coop_part, (int)kPartEmptyHi, doubles * 2));
-    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)c->d_coop_part, (int)kPartEmptyHi, doubles * 2, s));
     c->coop_part_cap = cap;
     c->coop_part_rows[0] = c->coop_part_rows[1] = 0;
     return YOUTH_OK;
@@ -3095,7 +3096,7 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
                        const PrepJob* job)
 {
     const int iters = c->prm.iters;
-    int rc = ensure_coop_part(c, n_pairs * G);
+    int rc = ensure_coop_part(c, s, n_pairs * G);
     if (rc) return rc;
     const int par = c->coop_par;
     unsigned* set = c->d_coop + (size_t)par * kCoopSetWords;
