@@ -2023,11 +2023,15 @@ constexpr int kCoopMaxPairs = 16;
 constexpr int kCoopBufs = 3;         // partial-row buffers per arena (iteration k % 3)
 constexpr unsigned kPartEmptyHi = 0x7FF7A5A5u;  // EMPTY = 0x7FF7A5A5'7FF7A5A5 (a signalling NaN)
 constexpr unsigned long long kPartEmpty = 0x7FF7A5A57FF7A5A5ull;
-// counter set layout (words): timeout word (one line) | [pair][32] prep-done
-// counters
+// counter set layout (words): timeout word (one line) | [pair][shard][32]
+// prep-done counters: workgroup c of a pair arrives on shard c % 8 (one
+// 128-B line each), so no line takes more than ~G/8 of the pair's arrivals
+// (MI355X_MICROARCH.md "fanin": 255 arrivals on one word take 3.2 us)
+constexpr int kCoopPrepShards = 8;
 constexpr int kCoopErrWord = 0;
 constexpr int kCoopPrepWords = kCoopErrWord + kCoopShardStride;
-constexpr int kCoopSetWords = kCoopPrepWords + kCoopMaxPairs * kCoopShardStride;
+constexpr int kCoopPrepPair = kCoopPrepShards * kCoopShardStride;  // words per pair
+constexpr int kCoopSetWords = kCoopPrepWords + kCoopMaxPairs * kCoopPrepPair;
 constexpr int kCoopTileH = 24;  // fused prep tiles: 64 x 24 pixels (one per workgroup of a 640x480 pair: 200 tiles, G = 200)
 constexpr int kCoopTileHTall = 80;  // 64 x 80 (= 10 px per lane x 512: one per workgroup of a 1280x960 pair, G = 240)
 constexpr unsigned kCoopSpinMax = 1u << 22;  // polls (~1 us each): seconds, never reached
@@ -2250,11 +2254,11 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
     const int c = blockIdx.x - p * G;
     const int N = W * H;
     unsigned* err = cs.set + kCoopErrWord;
-    unsigned* prep_cnt = cs.set + kCoopPrepWords + (size_t)p * kCoopShardStride;
+    unsigned* prep_cnt = cs.set + kCoopPrepWords + (size_t)p * kCoopPrepPair;
     // the prep counter this pair waits on: its own (prep_wait), or in a
     // tracker chain the previous pair's (whose prep is this pair's target)
     const bool prep_wait = cs.chain ? p > 0 : cs.prep_wait != 0;
-    unsigned* wait_cnt = cs.chain ? prep_cnt - kCoopShardStride : prep_cnt;
+    unsigned* wait_cnt = cs.chain ? prep_cnt - kCoopPrepPair : prep_cnt;
     const int tgt_frame = cs.chain ? cs.tgt_slot[p] : pm.tgt0 + p;
     float* X = coop_src;
     float* Y = coop_src + npx * kThreads;
@@ -2309,7 +2313,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
         __syncthreads();
         if ((cs.prep_wait || cs.chain) && threadIdx.x == 0)
-            __hip_atomic_fetch_add(prep_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(prep_cnt + (c & (kCoopPrepShards - 1)) * kCoopShardStride, 1u,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     COOP_MARK(0, 15);  // prep published
     // ---- this workgroup's source pixels, back-projected once (spec a2)
@@ -2350,22 +2355,31 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
     bool timeout = false;
     COOP_MARK(1, 15);  // source pixels staged
     if (cs.prep_src && prep_wait) {
-        // every workgroup of pair p prepped its tiles: ONE relaxed poll, ONE
-        // agent acquire (drops this CU's stale L1 lines), then plain gathers
-        if (threadIdx.x == 0) {
+        // every workgroup of pair p prepped its tiles: ONE relaxed poll (lane
+        // s of wave 0 polls shard s, which counts the chunks c = s mod 8),
+        // ONE agent acquire (drops this CU's stale L1 lines), then plain
+        // gathers
+        if (wave == 0) {
+            const unsigned want = lane < kCoopPrepShards
+                                      ? (unsigned)((G - lane + kCoopPrepShards - 1) / kCoopPrepShards)
+                                      : 0u;
             unsigned spins = 0;
             int stop = 0;
-            while (ld_u32_sc1(wait_cnt) < (unsigned)G) {
+            for (;;) {
+                const unsigned have =
+                    lane < kCoopPrepShards ? ld_u32_sc1(wait_cnt + lane * kCoopShardStride) : 0u;
+                if (__ballot(have < want) == 0ull) break;
                 __builtin_amdgcn_s_sleep(1);
                 if (++spins > cs.spin_max || ld_u32_sc1(err) != 0u) {
-                    __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (lane == 0)
+                        __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     stop = 1;
                     break;
                 }
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            sh_stop = stop;
+            if (lane == 0) sh_stop = stop;
         }
         __syncthreads();
         timeout = __builtin_amdgcn_readfirstlane(sh_stop) != 0;
