@@ -2233,7 +2233,6 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
                                                              const float4* __restrict__ recs,
                                                              size_t P, PairMap pm, int W, int H,
                                                              Intr K, FastK F, float thr2,
-                                                             double* __restrict__ partials,
                                                              CoopState cs)
 {
     extern __shared__ float coop_src[];  // [3][npx][kThreads]
@@ -2266,7 +2265,12 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
 
     COOP_MARK(3, 15);  // prologue stamps: kernel entry (slot 15 of iterations 3, 0, 1, 2)
     if (blockIdx.x == 0) {
-        for (int i = threadIdx.x; i < kCoopSetWords; i += kThreads) st_u32_sc1(cs.set_next + i, 0u);
+        // the next call's words: the timeout word and every prep shard word
+        // (word 0 of each 128-B line; the rest of a line is never used)
+        for (int i = threadIdx.x; i < 1 + kCoopMaxPairs * kCoopPrepShards; i += kThreads)
+            st_u32_sc1(cs.set_next + (i == 0 ? kCoopErrWord
+                                             : kCoopPrepWords + (i - 1) * kCoopShardStride),
+                       0u);
         if (threadIdx.x == 0) {
             st_u32_sc1(cs.head_err + kQError, 0u);
             st_u32_sc1(cs.head_err + kQSpins, 0u);
@@ -3164,9 +3168,8 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
     Intr K = c->K;
     FastK F = c->F;
     float thr2 = c->prm.dist_thresh * c->prm.dist_thresh;
-    double* partials = c->d_partials;
     void* args[] = {(void*)&dsrc, (void*)&recs, (void*)&P, (void*)&pm, (void*)&W, (void*)&H,
-                    (void*)&K, (void*)&F, (void*)&thr2, (void*)&partials, (void*)&cs};
+                    (void*)&K, (void*)&F, (void*)&thr2, (void*)&cs};
     EventPair ep{};
     rc = ev_begin(c, s, &ep, 0);
     if (rc) return rc;
