@@ -2213,7 +2213,12 @@ __device__ __forceinline__ void coop_group(const float* __restrict__ X, const fl
     f4v rec[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q)
-        rec[q] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rrec, (int)((unsigned)j[q] * 16u), 0, 0));
+        // aux 16 = sc1: the records come from this launch's fused prep (sc1
+        // stores, drained, sharded counter) and are read ONLY by sc1 loads, so
+        // no agent acquire is needed after the prep wait (MI355X_MICROARCH.md
+        // "Valid forms", table row 1; L1 hits were worth less than the
+        // acquire: C2 15.9 -> 16.4 K, profiles/r05/c2ab_r5zc_sc1_gathers.txt)
+        rec[q] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rrec, (int)((unsigned)j[q] * 16u), 0, 16));
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
         nmatch += __builtin_popcountll(match_accumulate<kSp, kFast, false>(
@@ -2360,9 +2365,9 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
     COOP_MARK(1, 15);  // source pixels staged
     if (cs.prep_src && prep_wait) {
         // every workgroup of pair p prepped its tiles: ONE relaxed poll (lane
-        // s of wave 0 polls shard s, which counts the chunks c = s mod 8),
-        // ONE agent acquire (drops this CU's stale L1 lines), then plain
-        // gathers
+        // s of wave 0 polls shard s, which counts the chunks c = s mod 8);
+        // the other waves load after the barrier below, and every gather of
+        // the records is an sc1 load (coop_group), so no acquire follows
         if (wave == 0) {
             const unsigned want = lane < kCoopPrepShards
                                       ? (unsigned)((G - lane + kCoopPrepShards - 1) / kCoopPrepShards)
@@ -2381,8 +2386,6 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
                     break;
                 }
             }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lane == 0) sh_stop = stop;
         }
         __syncthreads();
