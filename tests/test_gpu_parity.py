@@ -1528,3 +1528,25 @@ def test_coop_lost_row_times_out_and_context_recovers(monkeypatch):
             T64, _, st = ctx.get_poses(n)
             assert not st.any(), (n, st)
             assert np.array_equal(T64, want[n]), n
+
+
+@pytest.mark.parametrize("W,H", [(640, 480), (320, 240), (160, 120), (97, 53)])
+def test_coop_polled_rows_back_to_back(W, H):
+    """k_icp_coop's polled partial rows under load: 600 single-pair aligns
+    back to back on one stream (two arenas alternating, rows reset by the
+    next-but-one call, every iteration's wait on rows that are still landing),
+    every fp32 pose bit-identical to the first and no timeout."""
+    import torch
+    K = youth_icp.default_intrinsics(W, H)
+    src, dst, _ = youth_synth.pairs(61, 1, W, H)
+    ds, dd = torch.from_numpy(src).cuda(), torch.from_numpy(dst).cuda()
+    reps = 600
+    out = torch.zeros((reps, 16), device="cuda")
+    with youth_icp.IcpContext(W, H, 2, K=K) as ctx:
+        for r in range(reps):
+            ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), 1, d_T_out=out[r].data_ptr())
+        torch.cuda.synchronize()
+        assert ctx.get_plan()["kernel"] == "k_icp_coop"
+        assert not ctx.get_poses(1)[2].any()
+    rows = out.cpu().numpy()
+    assert (rows == rows[0]).all()
