@@ -12,7 +12,10 @@ import youth_synth  # noqa: E402
 
 src, dst, _ = youth_synth.pairs(7, 64)
 ds, dd = torch.from_numpy(src).cuda(), torch.from_numpy(dst).cuda()
-for n, iters in ((1, 1), (1, 2), (1, 10), (8, 10), (64, 10)):
+cases = ((1, 1), (1, 2), (1, 10), (8, 10), (64, 10))
+if len(sys.argv) > 2:
+    cases = ((int(sys.argv[1]), int(sys.argv[2])),)
+for n, iters in cases:
     with youth_icp.IcpContext(640, 480, 64, iters=iters) as ctx:
         t0 = time.time()
         ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), n)
