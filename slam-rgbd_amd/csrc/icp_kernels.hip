@@ -2148,9 +2148,13 @@ __device__ __forceinline__ double sum_pair_rows_polled(__amdgpu_buffer_rsrc_t rp
                 for (int i = 0; i < kBatch; ++i) {
                     if (v[i].y == kPartEmptyHi || v[i].w == kPartEmptyHi) {  // pad rows are 0
                         miss = true;
+                        // volatile (aux bit 31; emitted as sc0 sc1): the
+                        // optimiser must re-issue every re-poll (a non-volatile
+                        // one was once left out of a loop: DESIGN.md §9 1b)
                         v[i] = __builtin_bit_cast(
                             u4v, __builtin_amdgcn_raw_buffer_load_b128(
-                                     rpart, ((bb + i * kSumCols) * kPartStride + 2 * q) * 8, 0, 16));
+                                     rpart, ((bb + i * kSumCols) * kPartStride + 2 * q) * 8, 0,
+                                     (int)(16u | 0x80000000u)));
                     }
                 }
                 if (!miss) break;
