@@ -749,6 +749,15 @@ def single_pair_rate(R, d_src, d_dst, src0, dst0, steps=400, warmup=40):
            "value": steps / el, "unit": "aligns/s", "us_per_align": el / steps * 1e6,
            "steps": steps, "warmup": warmup, "kernel_path": ctx.get_plan(),
            "status": int(st[0]), "pose_max_abs_err_vs_cpu": pose_err(T1[0], T_cpu)}
+    # k_icp_coop is the whole align (one launch per call, back to back: the
+    # kernel trace shows no gaps, profiles/r05/c2_c3_kernel_trace_r5zm.txt)
+    nbytes = 18.0 * a.width * a.height * a.iters
+    gbs = nbytes / (el / steps) / 1e9
+    res["roofline"] = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": gbs / HBM_PEAK_GBS, "kernel": "k_icp_coop (target prep fused: "
+                       "its 18 B/px not counted)", "algorithmic_bytes_per_launch": nbytes,
+                       "algorithmic_model": "18 B per pixel-iteration x W x H x iters",
+                       "time": "wall clock per call over the timed calls"}
     ctx.close()
     return res
 
@@ -1306,6 +1315,48 @@ def cpu_baseline(a, src, dst, T_gpu):
     return cpu, parity
 
 
+def legs_summary(result):
+    """Every leg's headline in one compact object, emitted as the LAST key of
+    the bench line, so the driver's truncated stdout tail still carries them
+    (VERDICT r5 item 3).  Values are copied from the full legs above it."""
+    def get(*path):
+        x = result
+        for k in path:
+            if not isinstance(x, dict) or k not in x:
+                return None
+            x = x[k]
+        return x
+
+    def r(v, nd=4):
+        return None if v is None else float(f"{v:.{nd}g}")
+
+    sa = get("c5", "streamed", "slam_api")
+    legs = {
+        "c4": {"value": r(get("value")), "frac": r(get("roofline", "frac"), 3)},
+        "c2": {"value": r(get("c2", "value")), "us": r(get("c2", "us_per_align"), 3),
+               "frac": r(get("c2", "roofline", "frac"), 3)},
+        "c3_single": {"value": r(get("c3", "single_pair", "value")),
+                      "frac": r(get("c3", "single_pair", "roofline", "frac"), 3)},
+        "c3_batch": {"value": r(get("c3", "batch", "value")),
+                     "frac": r(get("c3", "batch", "roofline", "frac"), 3)},
+        "c5_batch": r(get("c5", "batch", "value")),
+        "c5_streamed": r(get("c5", "streamed", "value")),
+        "slam_api_py": r(get("c5", "streamed", "slam_api", "value")),
+        "slam_api_py_push_us": (None if not sa or "push_us_per_frame" not in sa else
+                                r(float(np.median(sa["push_us_per_frame"])), 3)),
+        "slam_api_c": r(get("c5", "streamed", "slam_api", "c_producer", "value")),
+        "slam_api_c_push_us": (None if not sa or "c_producer" not in sa or
+                               "push_us_per_frame" not in sa["c_producer"] else
+                               r(float(np.median(sa["c_producer"]["push_us_per_frame"])), 3)),
+        "spec_parity_max_vs_survey_oracle": r(get("spec_parity", "max_vs_survey_oracle",
+                                                  get("spec_parity", "default_variant") or "survey"), 3),
+        "parity_max_vs_cpu": r(get("parity", "pose_max_abs_err_vs_cpu"), 3),
+    }
+    if get("c2", "roofline", "frac") is None:
+        legs["c2"].pop("frac")
+    return legs
+
+
 def main():
     a = parse()
     os.environ["YOUTH_ICP_SPEC"] = a.spec   # every context of this run (youth_icp_create)
@@ -1318,6 +1369,7 @@ def main():
     with torch.cuda.stream(torch.cuda.Stream()):
         result = run_pairs(R) if a.workload == "pairs" else run_sequence(R)
     if R.rank == 0:
+        result["legs"] = legs_summary(result)   # last key: survives a truncated tail
         print(json.dumps(result), flush=True)
     R.finish()
     if R.rank == 0 and not result.get("parity_all_ranks_ok", True):

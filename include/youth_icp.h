@@ -409,6 +409,45 @@ int youth_icp_track_collect(youth_icp_ctx* ctx, double* T_rel, int* has_ref);
 /* Frames submitted and not yet collected (0 .. YOUTH_TRACK_MAX_IN_FLIGHT). */
 int youth_icp_track_pending(const youth_icp_ctx* ctx);
 
+/* What a tracked frame's status bits mean for its pose, and what to do:
+ *   YOUTH_STATUS_TIMEOUT      the align's cooperative grid was not co-resident
+ *                             (another process held CUs; k_icp_coop is launched
+ *                             as a plain kernel sized to an idle device) and its
+ *                             waits hit their spin bound: T_rel is a partly
+ *                             iterated pose and MUST NOT be used.  The frame's
+ *                             records (the next reference) are complete
+ *                             nevertheless: every workgroup preps its tiles
+ *                             before it waits, so the frames after it are
+ *                             unaffected.  Re-align it with
+ *                             youth_icp_track_realign (the SLAM worker and
+ *                             youth_icp_track_host_sequence do).
+ *   YOUTH_STATUS_FEW_MATCHES  some iteration had < 6 correspondences, or
+ *   YOUTH_STATUS_DEGENERATE   its 6x6 system was singular: that iteration's
+ *                             update was skipped, the others were applied.
+ *                             T_rel is the pose the remaining updates reached
+ *                             (identity when none was applied: the "no motion"
+ *                             estimate).  It is a valid, if weak, estimate: the
+ *                             SLAM worker composes it into the trajectory and
+ *                             records the status beside the pose
+ *                             (youth_slam_get_status).
+ *
+ * youth_icp_track_realign aligns depth (source, the timed-out frame) to
+ * ref_depth (target, the frame tracked before it), host int16 frames of the
+ * context's size, synchronously, and returns the status bits (>= 0) with
+ * T_rel (fp64 4x4, P_ref = T_rel P_new) or a negative YOUTH_E* code.  It
+ * first waits for everything the tracker has in flight (their results stay
+ * collectable), then runs the context's single-pair cooperative plan, which
+ * reproduces the undisturbed tracker's pose bit for bit; if that times out
+ * too, the persistent kernel, which needs no co-residency (the same pose up to
+ * fp64 summation order, ~1e-16 relative).  The tracker's reference and its
+ * frames in flight are not disturbed.  youth_icp_track_realigned counts the
+ * successful realigns on the cooperative plan (returned), on the persistent
+ * kernel (*persistent) and realigns that still timed out (*failed). */
+int youth_icp_track_realign(youth_icp_ctx* ctx, const int16_t* ref_depth,
+                            const int16_t* depth, const double* T_init, double* T_rel);
+long long youth_icp_track_realigned(const youth_icp_ctx* ctx, long long* persistent,
+                                    long long* failed);
+
 /* Micro-batch of n_frames consecutive host frames ([n_frames][H][W]) for a
  * backlogged stream: the same as n_frames youth_icp_track_submit calls
  * (T_init identity), each frame collected by its own youth_icp_track_collect
@@ -466,7 +505,9 @@ long long youth_icp_track_chained_frames(const youth_icp_ctx* ctx);
  * youth_icp_track_frame on each frame in order (continuing from the
  * reference the context holds).  T_rel [n][16] and status [n] (nullable)
  * receive the frames that had a reference, in order; returns how many, or a
- * negative YOUTH_E* code (nothing left in flight either way). */
+ * negative YOUTH_E* code (nothing left in flight either way).  A frame
+ * k >= 1 whose align timed out is realigned against frame k - 1
+ * (youth_icp_track_realign), so its entry is the undisturbed result. */
 int youth_icp_track_host_sequence(youth_icp_ctx* ctx, const int16_t* frames, int n_frames,
                                   double* T_rel, int32_t* status);
 
@@ -517,6 +558,21 @@ int youth_slam_wait_idle(int timeout_ms);
  * a backlogged queue; 0 when every frame arrived alone or with
  * YOUTH_SLAM_TRACK_BATCH=1). */
 long long youth_slam_batched_frames(void);
+/* Aligns the worker found timed out (YOUTH_STATUS_TIMEOUT) and realigned
+ * (youth_icp_track_realign): returns those the cooperative plan completed
+ * (bit-identical to an undisturbed run), *persistent those the persistent
+ * kernel completed, *lost those that still timed out.  A timed-out pose is
+ * never composed into the trajectory: a lost frame is left out of it, and the
+ * next frame composes onto the last recorded pose (no motion across the lost
+ * frame).  Counted since the module started. */
+long long youth_slam_realigned(long long* persistent, long long* lost);
+/* Status bits (YOUTH_STATUS_FEW_MATCHES / _DEGENERATE, never TIMEOUT) of the
+ * first n trajectory entries into status[n] (nullable), and the number of
+ * recorded frames with each bit since the module started (nullable).  Such a
+ * frame's pose is composed: it is the pose its applied updates reached
+ * (youth_icp_track_realign's comment).  Returns the count copied. */
+int youth_slam_get_status(int n, int32_t* status, long long* few_matches,
+                          long long* degenerate);
 /* Frames waiting in the module's ingest queue (processSlamFrame drops the
  * oldest down to 5 when it passes 10, SLAM.cpp:163-168): a producer that
  * must not lose frames waits while this is 10. */
@@ -529,9 +585,10 @@ void youth_slam_wait_stopped(void);
  * (CLOCK_MONOTONIC seconds, the clock rocprofv3 traces use) into a
  * fixed-size buffer, lock-free; events past the capacity are dropped.
  * youth_slam_trace_enable(0) stops recording and frees the buffer.  Enable
- * or disable only while no frame is being pushed.  youth_slam_trace_read
- * copies up to n events (t[n] seconds, kind[n], arg[n]) and returns how many
- * were recorded (at most the capacity; may exceed n).  Kinds and their arg: */
+ * or disable at any time (a buffer is freed only after every writer that may
+ * hold it has finished).  youth_slam_trace_read copies up to n events (t[n]
+ * seconds, kind[n], arg[n]) and returns how many were recorded and finished,
+ * in order (at most the capacity; may exceed n).  Kinds and their arg: */
 #define YOUTH_SLAM_EV_PUSH_BEGIN    1  /* queue depth before the push */
 #define YOUTH_SLAM_EV_PUSH_END      2  /* buffer: 0 pooled, 2 new pageable (1 unused: the
                                           producer never allocates page-locked memory) */
@@ -546,6 +603,8 @@ void youth_slam_wait_stopped(void);
 #define YOUTH_SLAM_EV_DROP          11 /* frames dropped by the >10 -> 5 policy */
 #define YOUTH_SLAM_EV_SUBMIT_STEP   12 /* inside a tracker submission: 1 slots ready, 2 waits
                                           enqueued, 3 H2D copies enqueued, 4 H2D event, 5 launch */
+#define YOUTH_SLAM_EV_REALIGN       13 /* a timed-out align realigned: 0 cooperative plan,
+                                          1 persistent kernel, 2 lost */
 int youth_slam_trace_enable(int capacity);
 int youth_slam_trace_read(int n, double* t, int* kind, int* arg);
 

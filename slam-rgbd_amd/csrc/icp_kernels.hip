@@ -2015,8 +2015,15 @@ __global__ __launch_bounds__(kRedThreads, 4) void k_icp(const int16_t* __restric
 // k+2 value, never the k-1 one.  Across calls the rows alternate between two
 // arenas with the counter sets: a call resets the rows the previous call
 // used in the other arena (stream order: the arena a call uses is never the
-// one it resets).  Co-residency is guaranteed by the cooperative launch;
-// every spin is still bounded (timeout -> YOUTH_STATUS_TIMEOUT, no hang).
+// one it resets).  Co-residency is NOT guaranteed: by default the grid is a
+// plain launch sized to an idle device's capacity (coop_enqueue orders this
+// process's cooperative launches per device; hipLaunchCooperativeKernel is
+// opt-in, YOUTH_ICP_COOP_LAUNCH=runtime), so another process holding CUs
+// can leave workgroups unscheduled.  Every spin is therefore bounded
+// (timeout -> YOUTH_STATUS_TIMEOUT, no hang), every workgroup preps its
+// tiles before it first waits (a timed-out launch still leaves complete
+// records), and the tracker realigns a timed-out frame
+// (youth_icp_track_realign: the same plan again, then the persistent k_icp).
 constexpr int kCoopShardStride = 32;  // words: one 128-B line per counter
 constexpr int kCoopMaxPx = 32;       // source pixels per lane (LDS: 3 x 32 KB)
 constexpr int kCoopMaxPairs = 16;
@@ -2682,7 +2689,9 @@ struct youth_icp_ctx {
     int coop_part_cap = 0;           // rows per buffer
     int coop_part_rows[2] = {0, 0};  // rows per buffer the last call on each arena used
     int coop_poll_delay = -1;        // YOUTH_ICP_COOP_POLL_DELAY (x 64 clocks); -1: G / 8
-    int coop_stall_once = -1;        // YOUTH_ICP_TEST_COOP_STALL (test hook, first coop launch only)
+    int coop_stall_once = -1;        // YOUTH_ICP_TEST_COOP_STALL (test hook): chunk that stalls
+    int coop_stall_left = 0;         // coop launches the hook still stalls
+    bool realign_stall = false;      // YOUTH_ICP_TEST_REALIGN_STALL=1 (test hook): realigns' coop launches stall
     int last_coop_G = 0, last_coop_px = 0;
     bool last_coop = false;          // the last align ran k_icp_coop
 
@@ -2696,6 +2705,7 @@ struct youth_icp_ctx {
     int trk_batch = 1;                // frames per submission in youth_icp_track_host_sequence
     long long trk_chained = 0;        // micro-batch launches so far (youth_icp_track_chained)
     long long trk_chained_frames = 0; // frames those launches aligned (youth_icp_track_chained_frames)
+    long long trk_realigned[3] = {};  // youth_icp_track_realign: coop / persistent / still failed
     int queues = 0;                  // k_icp work queues (YOUTH_ICP_QUEUES=1..8; 0: by batch size)
     int share = 1;                   // contexts launching k_icp concurrently (set_concurrency)
     int prep_xcd_map = 0;             // YOUTH_ICP_PREP_XCD_MAP=1: k_prep tiles contiguous per XCD (slower)
@@ -3164,11 +3174,12 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
     // 20-24, 1280x960 (G 240) at 28-32; no wait 13.7 K / 4.93 K aligns/s,
     // 24: 15.7 K / 5.32 K, 32: 15.3 K / 5.41 K; the tracker within noise)
     cs.poll_delay = c->coop_poll_delay >= 0 ? c->coop_poll_delay : G / 8;
-    // test hook (YOUTH_ICP_TEST_COOP_STALL=<chunk>): the context's first coop
-    // launch loses one row, so every wait times out after ~20 ms
+    // test hook (YOUTH_ICP_TEST_COOP_STALL=<chunk>[:<launches>]): the
+    // context's first coop launches lose one row, so their waits time out
+    // after ~20 ms
     cs.stall_chunk = c->coop_stall_once;
     cs.spin_max = c->coop_stall_once >= 0 ? 20000u : kCoopSpinMax;
-    c->coop_stall_once = -1;
+    if (c->coop_stall_once >= 0 && --c->coop_stall_left <= 0) c->coop_stall_once = -1;
     const float4* recs = c->d_rec;
     size_t P = c->P;
     int W = c->W, H = c->H;
@@ -3649,13 +3660,32 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
         if (pres && atoi(pres) >= 0) c->trk_pull_reserve = atoi(pres);
         const char* cpt = getenv("YOUTH_ICP_COPY_THREADS");
         if (cpt && atoi(cpt) >= 0) c->trk_copy_helpers = std::min(atoi(cpt), 15);
-        // test hook (tests/test_gpu_parity.py): every cooperative launch of
-        // this context is refused as the runtime would, exercising the
-        // persistent fallback of run_iterations
+        // test hooks (tests/): YOUTH_ICP_TEST_COOP_STALL=<chunk>[:<launches>]
+        // makes the context's first <launches> (default 1) cooperative
+        // launches lose chunk <chunk>'s iteration-1 row of pair 0, so they
+        // time out (the tracker's realign path); YOUTH_ICP_TEST_REFUSE_COOP=1
+        // refuses every cooperative launch as the runtime would (the
+        // persistent fallback of run_iterations).  Either one is announced on
+        // stderr: a stray variable must not pass for a device fault
         const char* cst = getenv("YOUTH_ICP_TEST_COOP_STALL");
-        if (cst && atoi(cst) >= 0) c->coop_stall_once = atoi(cst);
+        if (cst && atoi(cst) >= 0) {
+            c->coop_stall_once = atoi(cst);
+            const char* colon = strchr(cst, ':');
+            c->coop_stall_left = colon && atoi(colon + 1) > 0 ? atoi(colon + 1) : 1;
+            fprintf(stderr, "youth_icp: TEST HOOK YOUTH_ICP_TEST_COOP_STALL=%s active: the first %d "
+                            "cooperative launch(es) of this context time out\n",
+                    cst, c->coop_stall_left);
+        }
+        const char* rst = getenv("YOUTH_ICP_TEST_REALIGN_STALL");
+        c->realign_stall = rst && *rst && *rst != '0';
+        if (c->realign_stall)
+            fprintf(stderr, "youth_icp: TEST HOOK YOUTH_ICP_TEST_REALIGN_STALL active: the "
+                            "cooperative launch of every youth_icp_track_realign times out\n");
         const char* crf = getenv("YOUTH_ICP_TEST_REFUSE_COOP");
         c->coop_refuse = crf && *crf && *crf != '0';
+        if (c->coop_refuse)
+            fprintf(stderr, "youth_icp: TEST HOOK YOUTH_ICP_TEST_REFUSE_COOP active: cooperative "
+                            "launches of this context are refused\n");
         const char* nqs = getenv("YOUTH_ICP_QUEUES");
         if (nqs && atoi(nqs) >= 1 && atoi(nqs) <= kMaxQueues) c->queues = atoi(nqs);
         const char* pxm = getenv("YOUTH_ICP_PREP_XCD_MAP");
@@ -4605,6 +4635,79 @@ int youth_icp_track_pending(const youth_icp_ctx* c)
     return c ? c->trk_n : 0;
 }
 
+// A tracker align that came back with YOUTH_STATUS_TIMEOUT (its cooperative
+// grid was not co-resident: another process held CUs, or the test hook) is
+// aligned again here from host copies of its two frames, synchronously.
+// Everything the tracker has enqueued finishes first, so the depth slots
+// 0 / 1 and a record slot other than the reference's are free to use, and
+// the tracker continues afterwards as if nothing had happened (its reference
+// records are untouched; a timed-out launch still preps every tile of its
+// frames, because its workgroups prep before they wait).
+//   1. the context's own single-pair plan: the cooperative kernel preps the
+//      target and aligns, with the npx / G / tile mapping the tracker's
+//      single-frame and chained launches use, so a successful retry gives the
+//      pose the undisturbed launch would have, bit for bit;
+//   2. if that times out too, the persistent k_prep + k_icp, which waits only
+//      on workgroups that are running (no co-residency assumption): the same
+//      pose up to fp64 summation order (~1e-16 relative).
+int youth_icp_track_realign(youth_icp_ctx* c, const int16_t* ref_depth, const int16_t* depth,
+                            const double* T_init, double* T_rel)
+{
+    if (!c || !ref_depth || !depth || !T_rel)
+        return set_error(YOUTH_EINVAL, "track_realign: bad arguments");
+    if (T_init)
+        for (int i = 0; i < 16; ++i)
+            if (!std::isfinite(T_init[i]))
+                return set_error(YOUTH_EINVAL, "T_init: non-finite entry in pair 0");
+    int rc = bind_device(c);
+    if (rc) return rc;
+    hipStream_t s = c->stream;
+    HIP_TRY(hipStreamSynchronize(s));
+    if (c->xfer) HIP_TRY(hipStreamSynchronize(c->xfer));
+    const size_t N = c->N;
+    const int rslot = c->track_ref == 0 ? 1 : 0;
+    HIP_TRY(hipMemcpyAsync(c->d_depth, depth, N * sizeof(int16_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(c->d_depth + N, ref_depth, N * sizeof(int16_t), hipMemcpyHostToDevice, s));
+    const PrepJob job{c->d_depth + N, 1, rslot, true};
+    c->coop_res_host = nullptr;
+    int32_t st = YOUTH_STATUS_TIMEOUT;
+    for (int attempt = 0; attempt < 2 && (st & YOUTH_STATUS_TIMEOUT); ++attempt) {
+        const bool coop_was = c->coop;
+        if (attempt == 1) c->coop = false;  // the persistent kernel
+        if (attempt == 0 && c->realign_stall) {  // test hook: this coop launch loses a row
+            c->coop_stall_once = 0;
+            c->coop_stall_left = 1;
+        }
+        rc = run_iterations(c, s, c->d_depth, PairMap{0, rslot}, 1, T_init, nullptr, nullptr, &job);
+        const bool ran_coop = c->last_coop;
+        if (attempt == 1) c->coop = coop_was;
+        if (rc) return rc;
+        double T[16];
+        unsigned err = 0;
+        HIP_TRY(hipMemcpyAsync(T, c->d_T64, sizeof(T), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(&st, c->d_status, sizeof(st), hipMemcpyDeviceToHost, s));
+        if (!ran_coop)  // the persistent kernel's spin bound lands in the queue's error word
+            HIP_TRY(hipMemcpyAsync(&err, c->d_head + kQError, sizeof(err), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (err) st |= YOUTH_STATUS_TIMEOUT;
+        for (int i = 0; i < 12; ++i) T_rel[i] = T[i];
+        T_rel[12] = T_rel[13] = T_rel[14] = 0.0;
+        T_rel[15] = 1.0;
+        if (!(st & YOUTH_STATUS_TIMEOUT)) ++c->trk_realigned[ran_coop ? 0 : 1];
+        // a refused cooperative launch already ran the persistent path
+        if (!ran_coop) break;
+    }
+    if (st & YOUTH_STATUS_TIMEOUT) ++c->trk_realigned[2];
+    return st;
+}
+
+long long youth_icp_track_realigned(const youth_icp_ctx* c, long long* persistent, long long* failed)
+{
+    if (persistent) *persistent = c ? c->trk_realigned[1] : 0;
+    if (failed) *failed = c ? c->trk_realigned[2] : 0;
+    return c ? c->trk_realigned[0] : 0;
+}
+
 int youth_icp_track_host_sequence(youth_icp_ctx* c, const int16_t* frames, int n_frames,
                                   double* T_rel, int32_t* status)
 {
@@ -4612,12 +4715,22 @@ int youth_icp_track_host_sequence(youth_icp_ctx* c, const int16_t* frames, int n
         return set_error(YOUTH_EINVAL, "track_host_sequence: bad arguments");
     if (c->trk_n) return set_error(YOUTH_EINVAL, "track_host_sequence: submitted frames not collected");
     const size_t N = c->N;
-    int written = 0;
+    int written = 0, collected = 0;
     auto collect = [&]() -> int {
         double T[16];
         int has = 0;
-        const int st = youth_icp_track_collect(c, T, &has);
+        int st = youth_icp_track_collect(c, T, &has);
+        const int f = collected++;  // sequence index of the collected frame
         if (st < 0) return st;
+        // a timed-out align is aligned again against the frame before it
+        // (frame 0's reference came from an earlier call: its status keeps
+        // the TIMEOUT bit)
+        if (has && (st & YOUTH_STATUS_TIMEOUT) && f >= 1) {
+            const int st2 = youth_icp_track_realign(c, frames + (size_t)(f - 1) * N,
+                                                    frames + (size_t)f * N, nullptr, T);
+            if (st2 < 0) return st2;
+            st = st2;
+        }
         if (has) {
             memcpy(T_rel + (size_t)written * 16, T, sizeof(T));
             if (status) status[written] = st;

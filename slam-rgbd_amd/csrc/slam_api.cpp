@@ -36,15 +36,29 @@
 // ----------------------------------------------------------- event trace --
 // youth_slam_trace_enable / _read (youth_icp.h): timestamped events of the
 // producer and the worker in a fixed buffer, one fetch_add per event.
+// The buffer and its capacity are published together (one pointer), and a
+// buffer is freed only once no thread can still be writing into it: a writer
+// announces itself in g_tr_active before it loads the pointer it writes
+// through, and enable waits for the announced writers after swapping the
+// pointer (the worker traces on its own, e.g. idle wake-ups, so "no frame
+// being pushed" does not mean "no writer").  A slot is readable
+// once its writer has set `ready`.
 namespace {
 
 struct TraceEv {
     double t;
     int kind, arg;
+    std::atomic<int> ready{0};
 };
-std::atomic<TraceEv*> g_tr{nullptr};
-std::atomic<int> g_tr_n{0};
-int g_tr_cap = 0;
+struct TraceBuf {
+    explicit TraceBuf(int n) : cap(n), ev(new TraceEv[n]) {}
+    ~TraceBuf() { delete[] ev; }
+    const int cap;
+    TraceEv* const ev;
+    std::atomic<int> claimed{0};  // slots handed out (may pass cap: the buffer is full)
+};
+std::atomic<TraceBuf*> g_tr{nullptr};
+std::atomic<int> g_tr_active{0};  // writers between their announcement and their last store
 
 double mono_s()
 {
@@ -55,11 +69,20 @@ double mono_s()
 
 void trace(int kind, int arg)
 {
-    TraceEv* b = g_tr.load(std::memory_order_acquire);
-    // a full buffer stops counting (the count never wraps)
-    if (!b || g_tr_n.load(std::memory_order_relaxed) >= g_tr_cap) return;
-    const int i = g_tr_n.fetch_add(1, std::memory_order_relaxed);
-    if (i < g_tr_cap) b[i] = TraceEv{mono_s(), kind, arg};
+    if (!g_tr.load(std::memory_order_relaxed)) return;  // tracing off: no shared write
+    g_tr_active.fetch_add(1);                            // seq_cst: before the load below
+    TraceBuf* b = g_tr.load();
+    if (b && b->claimed.load(std::memory_order_relaxed) < b->cap) {
+        const int i = b->claimed.fetch_add(1, std::memory_order_relaxed);
+        if (i < b->cap) {
+            TraceEv& e = b->ev[i];
+            e.t = mono_s();
+            e.kind = kind;
+            e.arg = arg;
+            e.ready.store(1, std::memory_order_release);
+        }
+    }
+    g_tr_active.fetch_sub(1);
 }
 
 }  // namespace
@@ -225,20 +248,28 @@ int queue_prefill(youth_frame_queue* q, size_t n, int count)
     return added - freed;
 }
 
-// The worker's pass over a returned buffer: page-locked ones go back to the
-// pool; a pageable one (the producer found the pool empty) is freed and, while
-// fewer than `target` page-locked buffers exist, replaced by a page-locked one
-// of n values.  Returns 1 when it allocated one.
+// The worker's pass over a returned buffer: page-locked ones of at least n
+// values go back to the pool; a pageable one (the producer found the pool
+// empty), or a page-locked one smaller than the worker's frame size n (in
+// flight across a resolution change: pooled, it would count toward the
+// page-locked target forever and keep new-size buffers out), is
+// freed and, while fewer than `target` page-locked buffers exist, replaced
+// by a page-locked one of n values.  Returns 1 when it allocated one.
 int queue_release(youth_frame_queue* q, youth_frame_queue::Item& it, size_t n = 0, int target = 0)
 {
-    const bool was_pageable = it.buf && !it.pinned;
+    const bool replace = it.buf && (!it.pinned || (n > 0 && it.cap < n));
     std::vector<youth_frame_queue::Item> to_free;
     {
         std::lock_guard<std::mutex> lk(q->mu);
-        pool_put_locked(q, it, to_free);
+        if (it.buf && it.pinned && n > 0 && it.cap < n) {
+            to_free.push_back(it);
+            it.buf = nullptr;
+        } else {
+            pool_put_locked(q, it, to_free);
+        }
     }
     free_all(q, to_free);
-    if (!was_pageable || !q->pinned || n == 0) return 0;
+    if (!replace || !q->pinned || n == 0) return 0;
     {
         std::lock_guard<std::mutex> lk(q->mu);
         if (q->pinned_count >= target) return 0;
@@ -388,6 +419,7 @@ namespace {
 
 struct PoseRec {
     uint32_t ts;
+    int32_t status;  // the frame's YOUTH_STATUS_* bits (never TIMEOUT: such a frame is realigned or skipped)
     double T[16];
 };
 
@@ -398,6 +430,11 @@ std::atomic<bool> g_process{false};  // SLAM.cpp:29 process_frames
 std::atomic<bool> g_busy{false};
 std::atomic<bool> g_reset{false};
 std::atomic<long long> g_batched{0};  // frames tracked in micro-batches
+// timed-out aligns (YOUTH_STATUS_TIMEOUT): realigned on the cooperative plan,
+// on the persistent kernel, and lost (still timed out: not recorded)
+std::atomic<long long> g_realigned[3] = {};
+// recorded frames with YOUTH_STATUS_FEW_MATCHES / _DEGENERATE set
+std::atomic<long long> g_weak[2] = {};
 std::thread g_worker;
 youth_frame_queue* g_queue = nullptr;
 
@@ -443,13 +480,14 @@ youth_intrinsics intrinsics_for(int w, int h)
 
 // Frames per micro-batch of the worker (YOUTH_SLAM_TRACK_BATCH, default
 // YOUTH_TRACK_MAX_BATCH) and the page-locked buffers its queue keeps: a
-// backlog holds about queue (11) + in flight (2 batch) + one batch of frames.
+// backlog holds about queue (11) + in flight (2 batch) + one batch of frames,
+// plus the held reference frame (the target of a realign).
 int slam_batch()
 {
     const char* eb = getenv("YOUTH_SLAM_TRACK_BATCH");
     return eb ? std::max(1, std::min(atoi(eb), YOUTH_TRACK_MAX_BATCH)) : YOUTH_TRACK_MAX_BATCH;
 }
-int pool_target(int batch) { return 11 + 3 * batch; }
+int pool_target(int batch) { return 12 + 3 * batch; }
 
 // SLAM.cpp:32-63 processFramesThread, with TrackRGBD replaced by HIP ICP.
 // The worker takes every frame of the current size already queued behind
@@ -482,8 +520,20 @@ void worker_main(int device)
     };
     std::deque<Pending> pend;  // submitted, not yet collected (oldest first)
     int subs = 0;              // submissions in pend
+    // The last collected frame's buffer stays out of the pool until the next
+    // frame has been collected: it is the target a timed-out align of that
+    // frame is realigned against (youth_icp_track_realign).
+    Item ref_hold;
+    bool ref_valid = false;  // ref_hold is the tracker's reference of the next collected frame
+    auto drop_ref = [&]() {
+        if (ref_hold.buf && queue_release(g_queue, ref_hold, (size_t)cw * ch, pool_target(batch)))
+            trace(YOUTH_SLAM_EV_POOL, 1);
+        ref_hold = Item();
+        ref_valid = false;
+    };
     // collect the oldest submitted frame; record its pose unless a reset
-    // arrived since it was submitted; its buffer goes back to the pool
+    // arrived since it was submitted; it becomes the held reference and the
+    // previous one's buffer goes back to the pool
     auto finish_one = [&](bool record) {
         Pending pr0 = pend.front();
         pend.pop_front();
@@ -491,12 +541,41 @@ void worker_main(int device)
         double T_rel[16];
         int has_ref = 0;
         trace(YOUTH_SLAM_EV_COLLECT_BEGIN, (int)pend.size() + 1);
-        const int st = youth_icp_track_collect(ctx, T_rel, &has_ref);
+        int st = youth_icp_track_collect(ctx, T_rel, &has_ref);
         trace(YOUTH_SLAM_EV_COLLECT_END, pr0.last ? 1 : 0);
-        if (queue_release(g_queue, pr0.item, (size_t)cw * ch, pool_target(batch)))
-            trace(YOUTH_SLAM_EV_POOL, 1);
+        if (st >= 0 && has_ref && (st & YOUTH_STATUS_TIMEOUT)) {
+            // never composed: aligned again from the two frames' host buffers
+            // (the cooperative plan, bit-identical when it completes; else the
+            // persistent kernel); still timed out = lost
+            int how = 2;
+            if (ref_valid) {
+                long long p0 = 0, p1 = 0;
+                const long long c0 = youth_icp_track_realigned(ctx, &p0, nullptr);
+                const int st2 = youth_icp_track_realign(ctx, ref_hold.buf, pr0.item.buf, nullptr, T_rel);
+                const long long c1 = youth_icp_track_realigned(ctx, &p1, nullptr);
+                if (st2 < 0)
+                    fprintf(stderr, "youth_icp: realign failed: %s\n", youth_icp_last_error());
+                else
+                    st = st2;
+                how = c1 > c0 ? 0 : p1 > p0 ? 1 : 2;
+            }
+            g_realigned[how].fetch_add(1);
+            trace(YOUTH_SLAM_EV_REALIGN, how);
+        }
+        drop_ref();
         if (st < 0) {
+            if (queue_release(g_queue, pr0.item, (size_t)cw * ch, pool_target(batch)))
+                trace(YOUTH_SLAM_EV_POOL, 1);
             fprintf(stderr, "youth_icp: tracking failed: %s\n", youth_icp_last_error());
+            return;
+        }
+        ref_hold = pr0.item;
+        ref_valid = true;
+        if (st & YOUTH_STATUS_TIMEOUT) {
+            // no pose for this frame: it is left out of the trajectory and the
+            // next frame composes onto the last recorded pose (no motion
+            // across the lost frame)
+            fprintf(stderr, "youth_icp: frame %u lost (align timed out twice)\n", pr0.ts);
             return;
         }
         if (!record || g_reset.load()) return;
@@ -515,8 +594,14 @@ void worker_main(int device)
             // P_ref = T_rel P_new  =>  T_w_new = T_w_ref * T_rel
             mat_mul4(T_w_ref, T_rel, T_w_ref);
         }
+        // FEW_MATCHES / DEGENERATE: some iteration skipped its update; the pose
+        // the others reached is composed (identity motion if none applied)
+        // and the bits are kept with it (youth_slam_get_status)
+        if (st & YOUTH_STATUS_FEW_MATCHES) g_weak[0].fetch_add(1);
+        if (st & YOUTH_STATUS_DEGENERATE) g_weak[1].fetch_add(1);
         PoseRec pr;
         pr.ts = pr0.ts;
+        pr.status = st;
         memcpy(pr.T, T_w_ref, sizeof(pr.T));
         g_traj.push_back(pr);
         g_traj_len.store((int)g_traj.size(), std::memory_order_release);
@@ -554,10 +639,12 @@ void worker_main(int device)
         const int w = items[0].w, h = items[0].h;
         if (g_reset.exchange(false)) {
             while (!pend.empty()) finish_one(false);  // frames of the old sequence
+            drop_ref();
             if (ctx) youth_icp_track_reset(ctx);
         }
         if (!ctx || w != cw || h != ch) {
             while (!pend.empty()) finish_one(true);
+            drop_ref();
             if (ctx) youth_icp_destroy(ctx);
             const youth_intrinsics K = intrinsics_for(w, h);
             ctx = youth_icp_create(device, w, h, 2 * batch, &K, nullptr);
@@ -641,6 +728,7 @@ void worker_main(int device)
         if (batch == 1 && pend.size() == 2) finish_one(true);
     }
     while (ctx && !pend.empty()) finish_one(true);
+    drop_ref();
     if (held) queue_release(g_queue, held_item);
     if (ctx) youth_icp_destroy(ctx);
     fprintf(stderr, "youth_icp: SLAM processing thread stopped\n");
@@ -753,6 +841,8 @@ void initSlamModule(const char* config_file, const char* vocabulary_file)
     g_last_points = 0;
     g_process.store(true);
     g_batched.store(0);
+    for (auto& r : g_realigned) r.store(0);
+    for (auto& r : g_weak) r.store(0);
     try {
         g_worker = std::thread(worker_main, device);
     } catch (const std::exception& ex) {
@@ -880,6 +970,24 @@ int youth_slam_get_pose(int index, uint32_t* timestamp, double* T_wc)
 
 long long youth_slam_batched_frames(void) { return g_batched.load(); }
 
+long long youth_slam_realigned(long long* persistent, long long* lost)
+{
+    if (persistent) *persistent = g_realigned[1].load();
+    if (lost) *lost = g_realigned[2].load();
+    return g_realigned[0].load();
+}
+
+int youth_slam_get_status(int n, int32_t* status, long long* few_matches, long long* degenerate)
+{
+    if (few_matches) *few_matches = g_weak[0].load();
+    if (degenerate) *degenerate = g_weak[1].load();
+    std::lock_guard<std::mutex> lk(g_slam_mu);
+    int m = (int)g_traj.size();
+    if (n < m) m = n;
+    for (int i = 0; i < m && status; ++i) status[i] = g_traj[i].status;
+    return m;
+}
+
 int youth_slam_queue_size(void) { return g_queue ? youth_queue_size(g_queue) : 0; }
 
 int youth_slam_wait_idle(int timeout_ms)
@@ -901,33 +1009,41 @@ int youth_slam_wait_idle(int timeout_ms)
 // recorded from inside the tracker (icp_kernels.hip: a submission's steps)
 void youth_slam_trace_hook(int kind, int arg) { trace(kind, arg); }
 
+// enable / read are serialised against each other (the writers never take it)
+std::mutex g_tr_mu;
+
 int youth_slam_trace_enable(int capacity)
 {
     if (capacity < 0) return YOUTH_EINVAL;
-    TraceEv* old = g_tr.exchange(nullptr, std::memory_order_acq_rel);
-    delete[] old;
-    g_tr_n.store(0, std::memory_order_relaxed);
-    g_tr_cap = 0;
-    if (capacity == 0) return YOUTH_OK;
-    TraceEv* b = new (std::nothrow) TraceEv[capacity];
-    if (!b) return YOUTH_ENOMEM;
-    g_tr_cap = capacity;
-    g_tr.store(b, std::memory_order_release);
+    TraceBuf* b = nullptr;
+    if (capacity > 0) {
+        b = new (std::nothrow) TraceBuf(capacity);
+        if (!b) return YOUTH_ENOMEM;
+    }
+    std::lock_guard<std::mutex> lk(g_tr_mu);
+    TraceBuf* old = g_tr.exchange(b);  // seq_cst: after it, new writers see b
+    // a writer that may still hold `old` has announced itself before loading it
+    while (g_tr_active.load() != 0) std::this_thread::yield();
+    delete old;
     return YOUTH_OK;
 }
 
 int youth_slam_trace_read(int n, double* t, int* kind, int* arg)
 {
-    TraceEv* b = g_tr.load(std::memory_order_acquire);
-    const int rec = g_tr_n.load(std::memory_order_acquire);
+    std::lock_guard<std::mutex> lk(g_tr_mu);  // the buffer is not swapped meanwhile
+    TraceBuf* b = g_tr.load();
     if (!b) return 0;
-    const int m = std::min(std::min(n, rec), g_tr_cap);
+    const int claimed = std::min(b->claimed.load(std::memory_order_relaxed), b->cap);
+    // the events whose writers have finished, up to the first unfinished one
+    int done = 0;
+    while (done < claimed && b->ev[done].ready.load(std::memory_order_acquire)) ++done;
+    const int m = std::min(n, done);
     for (int i = 0; i < m; ++i) {
-        if (t) t[i] = b[i].t;
-        if (kind) kind[i] = b[i].kind;
-        if (arg) arg[i] = b[i].arg;
+        if (t) t[i] = b->ev[i].t;
+        if (kind) kind[i] = b->ev[i].kind;
+        if (arg) arg[i] = b->ev[i].arg;
     }
-    return rec;
+    return done;
 }
 
 void youth_slam_wait_stopped(void)

@@ -168,6 +168,13 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         "youth_slam_wait_stopped": (None, []),
         "youth_slam_trace_enable": (c_int, [c_int]),
         "youth_slam_trace_read": (c_int, [c_int, PD, POINTER(c_int), POINTER(c_int)]),
+        "youth_icp_track_realign": (c_int, [c_void_p, P16, P16, PD, PD]),
+        "youth_icp_track_realigned": (ctypes.c_longlong, [c_void_p, POINTER(ctypes.c_longlong),
+                                                          POINTER(ctypes.c_longlong)]),
+        "youth_slam_realigned": (ctypes.c_longlong, [POINTER(ctypes.c_longlong),
+                                                     POINTER(ctypes.c_longlong)]),
+        "youth_slam_get_status": (c_int, [c_int, PI32, POINTER(ctypes.c_longlong),
+                                          POINTER(ctypes.c_longlong)]),
     }
     ab_build = bool(os.environ.get("YOUTH_ICP_LIB"))  # tools/ab_*.sh: older builds
     for name, (res, args) in sig.items():
@@ -279,7 +286,8 @@ def slam_queue_size() -> int:
 
 SLAM_EVENTS = {1: "push_begin", 2: "push_end", 3: "take", 4: "submit_begin", 5: "submit_end",
                6: "collect_begin", 7: "collect_end", 8: "idle_begin", 9: "idle_end",
-               10: "pool", 11: "drop", 12: "submit_step"}   # YOUTH_SLAM_EV_* (youth_icp.h)
+               10: "pool", 11: "drop", 12: "submit_step",
+               13: "realign"}   # YOUTH_SLAM_EV_* (youth_icp.h)
 
 
 def slam_trace_enable(capacity: int) -> None:
@@ -295,6 +303,25 @@ def slam_trace_read(n: int = 1 << 20) -> tuple[np.ndarray, np.ndarray, np.ndarra
     m = min(n, load_library().youth_slam_trace_read(n, _p(t, c_double), _p(k, c_int),
                                                      _p(a, c_int)))
     return t[:m], k[:m], a[:m]
+
+
+def slam_realigned() -> dict:
+    """youth_slam_realigned: timed-out aligns the worker realigned on the
+    cooperative plan / the persistent kernel, and those it lost."""
+    p, lost = ctypes.c_longlong(0), ctypes.c_longlong(0)
+    coop = load_library().youth_slam_realigned(ctypes.byref(p), ctypes.byref(lost))
+    return {"coop": int(coop), "persistent": int(p.value), "lost": int(lost.value)}
+
+
+def slam_status() -> tuple[np.ndarray, int, int]:
+    """youth_slam_get_status: (status bits per trajectory entry, frames with
+    FEW_MATCHES, frames with DEGENERATE)."""
+    lib = load_library()
+    n = lib.youth_slam_trajectory_length()
+    st = np.zeros(max(n, 1), np.int32)
+    few, deg = ctypes.c_longlong(0), ctypes.c_longlong(0)
+    m = lib.youth_slam_get_status(n, _p(st, c_int32), ctypes.byref(few), ctypes.byref(deg))
+    return st[:m], int(few.value), int(deg.value)
 
 
 def slam_trajectory() -> tuple[np.ndarray, np.ndarray]:
@@ -611,6 +638,25 @@ class IcpContext:
 
     def track_pending(self) -> int:
         return int(self._lib.youth_icp_track_pending(self._ctx))
+
+    def track_realign(self, ref_depth: np.ndarray, depth: np.ndarray, T_init=None):
+        """(T_rel, status) of depth aligned to ref_depth again after a timed-out
+        tracker align (youth_icp_track_realign): the cooperative plan first
+        (bit-identical to an undisturbed align), the persistent kernel if that
+        times out too.  Waits for the frames in flight; leaves them collectable."""
+        r, _ = self._frame_args(ref_depth, None)
+        d, Ti = self._frame_args(depth, T_init)
+        T = np.zeros((4, 4), np.float64)
+        st = _check(self._lib.youth_icp_track_realign(self._ctx, _p(r, c_int16), _p(d, c_int16),
+                                                      _p(Ti, c_double), _p(T, c_double)))
+        return T, st
+
+    def track_realigned(self) -> dict:
+        """Realigns that completed on the cooperative plan / the persistent
+        kernel, and those that still timed out."""
+        p, f = ctypes.c_longlong(0), ctypes.c_longlong(0)
+        coop = self._lib.youth_icp_track_realigned(self._ctx, ctypes.byref(p), ctypes.byref(f))
+        return {"coop": int(coop), "persistent": int(p.value), "failed": int(f.value)}
 
     def track_host_sequence(self, frames: np.ndarray):
         """youth_icp_track_host_sequence: (T_rel [m, 4, 4], status [m]) of the

@@ -11,7 +11,11 @@
 //      from another thread;
 //   5. the same loop over POSIX queues (youth_algorithm_loop), when the
 //      machine allows them;
-//   6. stopSlamModule while producers are still pushing.
+//   6. stopSlamModule while producers are still pushing;
+//   7. timed-out aligns (the stub's YOUTH_STUB_TIMEOUT_EVERY) realigned by
+//      the worker, with the event trace enabled, read and disabled from
+//      another thread while the worker records (a freed trace
+//      buffer must never be written).
 // Exit 0 when every check holds; the sanitizers abort (exit 66 / non-zero)
 // on a report.
 #include <stdio.h>
@@ -262,12 +266,62 @@ static void scenario_stop_under_load()
     for (auto& p : prod) p.join();
 }
 
+static void scenario_realign_and_trace()
+{
+    stopSlamModule();
+    setenv("YOUTH_STUB_TIMEOUT_EVERY", "3", 1);
+    initSlamModule(nullptr, nullptr);
+    std::atomic<bool> done{false};
+    std::thread tracer([&] {
+        std::vector<double> t(256);
+        std::vector<int> k(256), a(256);
+        for (int i = 0; !done.load(); ++i) {
+            check(youth_slam_trace_enable(i % 3 == 2 ? 0 : 64 + 32 * (i % 5)) == 0, "trace enable");
+            (void)youth_slam_trace_read(256, t.data(), k.data(), a.data());
+            std::this_thread::sleep_for(std::chrono::microseconds(150));
+        }
+    });
+    const int F = 40;
+    long long want = 0;
+    for (int k = 0; k < F; ++k) {
+        auto f = frame(100 + 7 * k);
+        while (youth_slam_queue_size() >= 10) std::this_thread::yield();
+        check(processSlamFrame(f.data(), nullptr, W, H, (uint32_t)k) == 1, "processSlamFrame accepted");
+        if (k % 5 == 0) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+    check(youth_slam_wait_idle(20000) == 1, "worker idle");
+    done.store(true);
+    tracer.join();
+    check(youth_slam_trace_enable(0) == 0, "trace off");
+    long long persistent = -1, lost = -1;
+    const long long realigned = youth_slam_realigned(&persistent, &lost);
+    check(realigned >= F / 3 - 1 && persistent == 0 && lost == 0, "timed-out aligns realigned");
+    // every frame recorded, the last pose the sum of the stub's translations
+    // (7 mm steps x W x H values x 1e-6 per frame): no timed-out pose composed
+    const int len = youth_slam_trajectory_length();
+    check(len == F, "every frame recorded");
+    std::vector<uint32_t> ts(F);
+    std::vector<double> T((size_t)F * 16);
+    check(youth_slam_get_trajectory(F, ts.data(), T.data()) == F, "trajectory");
+    want = (long long)(F - 1) * 7 * W * H;
+    check(T[(size_t)(F - 1) * 16 + 3] > 0.999999 * want * 1e-6 &&
+              T[(size_t)(F - 1) * 16 + 3] < 1.000001 * want * 1e-6,
+          "trajectory composed from realigned poses");
+    std::vector<int32_t> st(F, -1);
+    check(youth_slam_get_status(F, st.data(), nullptr, nullptr) == F, "status");
+    for (int i = 0; i < F; ++i) check(st[i] == 0, "no TIMEOUT bit recorded");
+    stopSlamModule();
+    unsetenv("YOUTH_STUB_TIMEOUT_EVERY");
+    initSlamModule(nullptr, nullptr);  // scenario_stop_under_load stops it
+}
+
 int main()
 {
     scenario_init_and_producers();
     scenario_queue();
     scenario_frame_loop();
     scenario_mq_loop();
+    scenario_realign_and_trace();
     scenario_stop_under_load();
     printf("sanitizer driver: all scenarios passed\n");
     return 0;

@@ -4,15 +4,19 @@
  * (slam_api.cpp's worker: create / destroy / track_submit / track_collect /
  * track_frame / track_reset / track_submit_batch / track_set_batch /
  * track_chained / track_chained_frames / track_submit_pinned /
- * host_alloc / host_free / device_count / last_error, plus
- * youth_default_intrinsics), so the SLAM.h
+ * host_alloc / host_free / device_count / last_error / track_realign /
+ * track_realigned, plus youth_default_intrinsics), so the SLAM.h
  * queue + worker, the AlgorithmModule frame loop and the POSIX-queue
  * transport can run under ThreadSanitizer / AddressSanitizer on a machine
  * without a GPU (SURVEY §5 "Race detection").  It is linked only into the
  * sanitizer driver (tests/tsan/Makefile), never into libyouth_icp.so, and
  * computes no ICP: the "relative pose" is a translation derived from the
  * frame's depth sum, enough for the driver to check that every frame reached
- * the trajectory in order.
+ * the trajectory in order.  YOUTH_STUB_TIMEOUT_EVERY=k (read at create)
+ * makes every k-th frame with a reference come back YOUTH_STATUS_TIMEOUT with
+ * a wrong pose, as a timed-out cooperative align does, so the worker's
+ * realign path runs too; youth_icp_track_realign recomputes the pose from the
+ * two frames it is given.
  */
 #include <stdlib.h>
 #include <string.h>
@@ -32,6 +36,9 @@ struct youth_icp_ctx {
      * flight fails the run) */
     const int16_t* src[YOUTH_TRACK_MAX_IN_FLIGHT];
     long long src_sum[YOUTH_TRACK_MAX_IN_FLIGHT];
+    int status[YOUTH_TRACK_MAX_IN_FLIGHT];
+    int timeout_every, tracked;
+    long long realigned;
 };
 
 static long long depth_sum(const youth_icp_ctx* c, const int16_t* d)
@@ -63,6 +70,8 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
     (void)device, (void)max_frames, (void)K, (void)P;
     youth_icp_ctx* c = (youth_icp_ctx*)calloc(1, sizeof(*c));
     if (c) c->W = W, c->H = H;
+    const char* e = getenv("YOUTH_STUB_TIMEOUT_EVERY");
+    if (c && e) c->timeout_every = atoi(e);
     return c;
 }
 
@@ -77,9 +86,32 @@ int youth_icp_track_submit(youth_icp_ctx* c, const int16_t* depth, const double*
     if (c->n >= YOUTH_TRACK_MAX_IN_FLIGHT) return YOUTH_EINVAL;
     const int j = (c->head + c->n) % YOUTH_TRACK_MAX_IN_FLIGHT;
     stub_track(c, depth, c->T[j], &c->has[j]);
+    c->status[j] = 0;
+    if (c->has[j] && c->timeout_every > 0 && ++c->tracked % c->timeout_every == 0) {
+        c->status[j] = YOUTH_STATUS_TIMEOUT;
+        c->T[j][3] = 1e9; /* a partly iterated pose: must never reach the trajectory */
+    }
     c->src[j] = NULL;
     ++c->n;
     return 0;
+}
+
+int youth_icp_track_realign(youth_icp_ctx* c, const int16_t* ref_depth, const int16_t* depth,
+                            const double* T_init, double* T_rel)
+{
+    (void)T_init;
+    memset(T_rel, 0, 16 * sizeof(double));
+    T_rel[0] = T_rel[5] = T_rel[10] = T_rel[15] = 1.0;
+    T_rel[3] = (double)(depth_sum(c, depth) - depth_sum(c, ref_depth)) * 1e-6;
+    ++c->realigned;
+    return 0;
+}
+
+long long youth_icp_track_realigned(const youth_icp_ctx* c, long long* persistent, long long* failed)
+{
+    if (persistent) *persistent = 0;
+    if (failed) *failed = 0;
+    return c->realigned;
 }
 
 int youth_icp_track_collect(youth_icp_ctx* c, double* T_rel, int* has_ref)
@@ -90,9 +122,10 @@ int youth_icp_track_collect(youth_icp_ctx* c, double* T_rel, int* has_ref)
     if (c->src[c->head] && depth_sum(c, c->src[c->head]) != c->src_sum[c->head]) abort();
     memcpy(T_rel, c->T[c->head], 16 * sizeof(double));
     if (has_ref) *has_ref = c->has[c->head];
+    const int st = c->status[c->head];
     c->head = (c->head + 1) % YOUTH_TRACK_MAX_IN_FLIGHT;
     --c->n;
-    return 0;
+    return st;
 }
 
 int youth_icp_track_pending(const youth_icp_ctx* c) { return c->n; }
