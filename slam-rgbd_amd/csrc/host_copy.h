@@ -12,6 +12,9 @@
 // no helper still holds the job (a late helper can never see the next one).
 #pragma once
 
+#include <emmintrin.h>
+#include <stdint.h>
+
 #include <atomic>
 #include <condition_variable>
 #include <cstddef>
@@ -21,6 +24,33 @@
 #include <vector>
 
 namespace youth {
+
+// memcpy with non-temporal (streaming) 16-byte stores for the destination:
+// a frame copied into a page-locked queue buffer is next read by the GPU
+// (k_pull_frames / the H2D), not by this CPU, so the stores skip the
+// read-for-ownership of each destination line and leave the bytes in memory
+// rather than in this core's caches.  The sfence orders the streaming stores
+// before anything the caller publishes after it (the queue push under its
+// mutex).  SSE2 only (every x86-64).
+inline void stream_copy(void* dst, const void* src, size_t bytes)
+{
+    char* d = static_cast<char*>(dst);
+    const char* s = static_cast<const char*>(src);
+    size_t head = (16 - ((uintptr_t)d & 15)) & 15;
+    if (head > bytes) head = bytes;
+    memcpy(d, s, head);
+    d += head;
+    s += head;
+    bytes -= head;
+    size_t i = 0;
+    for (; i + 128 <= bytes; i += 128) {
+        __m128i v[8];
+        for (int k = 0; k < 8; ++k) v[k] = _mm_loadu_si128(reinterpret_cast<const __m128i*>(s + i + 16 * k));
+        for (int k = 0; k < 8; ++k) _mm_stream_si128(reinterpret_cast<__m128i*>(d + i + 16 * k), v[k]);
+    }
+    memcpy(d + i, s + i, bytes - i);
+    _mm_sfence();
+}
 
 class HostCopyPool {
 public:

@@ -31,6 +31,7 @@
 #include <thread>
 #include <vector>
 
+#include "host_copy.h"
 #include "youth_icp.h"
 
 // ----------------------------------------------------------- event trace --
@@ -122,6 +123,9 @@ struct youth_frame_queue {
     std::vector<Item> pool;
     int high = 10, low = 5;
     bool pinned = false;      // page-locked buffers (SLAM module queue), allocated off the producer path
+    // the producer's copy (youth_queue_push): 1 streaming stores
+    // (youth::stream_copy; YOUTH_SLAM_PUSH_COPY=nt), 0 memcpy (=memcpy)
+    int copy_mode = 1;
     size_t pinned_bytes = 0;  // page-locked bytes allocated and not freed
     int pinned_count = 0;     // page-locked buffers allocated and not freed
 };
@@ -291,6 +295,7 @@ youth_frame_queue* youth_queue_create(int high_water, int low_water)
     auto* q = new youth_frame_queue();
     q->high = high_water;
     q->low = low_water;
+    if (const char* e = getenv("YOUTH_SLAM_PUSH_COPY")) q->copy_mode = strcmp(e, "memcpy") == 0 ? 0 : 1;
     return q;
 }
 
@@ -314,7 +319,10 @@ int youth_queue_push(youth_frame_queue* q, const int16_t* depth, int width, int 
     int kind = 0;
     trace(YOUTH_SLAM_EV_PUSH_BEGIN, youth_queue_size(q));
     if (!buf_get(q, n, it, &kind)) return YOUTH_ENOMEM;
-    memcpy(it.buf, depth, n * sizeof(int16_t));
+    if (q->copy_mode == 1)
+        youth::stream_copy(it.buf, depth, n * sizeof(int16_t));
+    else
+        memcpy(it.buf, depth, n * sizeof(int16_t));
     it.w = width;
     it.h = height;
     it.ts = timestamp;

@@ -215,3 +215,61 @@ def test_bench_gpus_flag_self_launches_ranks():
     assert d["ranks"]["rccl_world_size"] == 2 and d["ranks"]["backend"] == "gloo"
     assert d["config"]["pairs_per_gpu"] == 32
     _assert_rank_parity(d, 2, 4)
+
+
+@pytest.mark.parametrize("workload", ["pairs", "sequence"])
+def test_bench_eight_ranks_rehearsal(workload, tmp_path):
+    """The driver's N = 8 run, rehearsed on one GPU:
+    `python bench.py --gpus 8` self-launches 8 ranks (gloo, so all of them
+    share the one device) on the real shard geometry: pairs with
+    --global-pairs 136 (17 per rank: the persistent path), and the C5
+    sequence with --frames 1000 (ranges of 125/124 pairs with a 1-frame
+    halo).  Every rank reports, every rank's parity sample passes, and the
+    poses the 8 ranks computed (fp64, dumped per rank) equal the N = 1 run's
+    within 1e-9 (the shards' launch shapes change only fp64 summation
+    order); for the sequence, rank 0's gathered and composed 1000-frame
+    trajectory too."""
+    import time
+
+    import numpy as np
+    env = dict(os.environ, YOUTH_BENCH_BACKEND="gloo", OMP_NUM_THREADS="2")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    common = ["--steps", "3", "--warmup", "1", "--windows", "1", "--workload", workload,
+              "--global-pairs", "136", "--frames", "1000", "--min-warmup-ms", "0"]
+    solo = ["--no-legs", "--no-cpu-baseline", "--no-host-io", "--no-viewer", "--no-spec-parity"]
+    p8, p1 = str(tmp_path / "n8"), str(tmp_path / "n1")
+    t0 = time.perf_counter()
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "8", "--dump-poses", p8] + common,
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+    wall8 = time.perf_counter() - t0
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    print(f"\n8-rank {workload} rehearsal: wall {wall8:.1f} s, value {d['value']:.0f} aligns/s")
+    assert d["n_gpus"] == 8 and d["value"] > 0 and d["scaling"] == "strong"
+    rk = d["ranks"]
+    assert rk["rccl_world_size"] == 8 and rk["backend"] == "gloo" and rk["gather_timed"]
+    for k in ("k_icp_ms", "k_prep_ms", "gather_ms"):
+        assert len(rk["per_rank_ms"][k]) == 8, k
+    assert min(rk["per_rank_ms"]["k_icp_ms"]) > 0
+    _assert_rank_parity(d, 8, 4 if workload == "pairs" else 2)
+    if workload == "pairs":
+        assert d["config"]["global_pairs"] == 136 and d["config"]["pairs_per_gpu"] == 17
+    else:
+        assert d["config"]["pairs"] == 999 and d["trajectory_frames"] == 1000
+    env1 = dict(env, OMP_NUM_THREADS="16")
+    r1 = subprocess.run([sys.executable, "bench.py", "--dump-poses", p1] + common + solo,
+                        cwd=ROOT, env=env1, capture_output=True, text=True, timeout=900)
+    assert r1.returncode == 0, r1.stderr[-3000:]
+    T8 = np.concatenate([np.load(f"{p8}.rank{k}.npy") for k in range(8)])
+    T1 = np.load(f"{p1}.rank0.npy")
+    want = 136 if workload == "pairs" else 999
+    assert T8.shape == T1.shape == (want, 4, 4)
+    err = float(np.abs(T8[:, :3, :] - T1[:, :3, :]).max())
+    assert err <= 1e-9, err
+    if workload == "sequence":
+        # rank 0's trajectory from the gathered fp32 relative poses against the
+        # N = 1 run's (each fp32 pose may round differently: a few 1e-8)
+        tr8, tr1 = np.load(f"{p8}.traj.npy"), np.load(f"{p1}.traj.npy")
+        assert tr8.shape == tr1.shape == (1000, 4, 4)
+        assert float(np.abs(tr8[:, :3, :] - tr1[:, :3, :]).max()) <= 1e-5
