@@ -1445,8 +1445,8 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
         for (int q = 0; q < 4; ++q) {
             LaneMask okm;
             if constexpr (sp_lane32(kSp))
-                okm = match_accumulate<kSp, kFast, true>(qx[q], qy[q], qz[q], t[q], fu[q], fv[q],
-                                                         in[q], K, F, thr2, facc);
+                okm = match_accumulate<kSp, kFast, false>(qx[q], qy[q], qz[q], t[q], fu[q], fv[q],
+                                                          in[q], K, F, thr2, facc);
             else
                 okm = match_accumulate<kSp, kFast, true>(qx[q], qy[q], qz[q], t[q], fu[q], fv[q],
                                                          in[q], K, F, thr2, acc);
@@ -1454,6 +1454,7 @@ __device__ __forceinline__ void accumulate_chunk(const int16_t* __restrict__ sD,
             // matches counted per wave on the scalar unit (s_bcnt1 of the
             // match mask) instead of a per-lane select and add
             cnt += __builtin_popcountll(okm);
+
         }
     }
     if constexpr (sp_lane32(kSp)) {

@@ -17,6 +17,7 @@ O=gpurun_out
 mkdir -p $O
 TAG=$1
 shift
+nb=0
 for step in "$@"; do
   name=${step%%:*}
   arg=${step#*:}
@@ -33,8 +34,9 @@ for step in "$@"; do
         > $O/smoke_$TAG.txt 2>&1 || { cat $O/smoke_$TAG.txt; exit 3; } ;;
     bench)
       IFS=, read -r -a ba <<< "$arg"
-      timeout -k 10 400 python -u bench.py "${ba[@]}" > $O/bench_$TAG.json 2> $O/bench_$TAG.err \
-        || { tail -30 $O/bench_$TAG.err; exit 4; } ;;
+      nb=$((nb + 1)); bt=$TAG; [ $nb -gt 1 ] && bt=${TAG}_$nb   # one file per bench step
+      timeout -k 10 400 python -u bench.py "${ba[@]}" > $O/bench_$bt.json 2> $O/bench_$bt.err \
+        || { tail -30 $O/bench_$bt.err; exit 4; } ;;
     profile)
       tools/profile.sh $TAG > $O/profile_$TAG.log 2>&1 || { tail -30 $O/profile_$TAG.log; exit 5; } ;;
     py)
