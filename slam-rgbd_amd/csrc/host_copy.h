@@ -60,7 +60,9 @@ public:
         size_t bytes;
     };
 
-    explicit HostCopyPool(int helpers)
+    // stream: pieces copied with youth::stream_copy (a destination no CPU
+    // reads next), else memcpy
+    explicit HostCopyPool(int helpers, bool stream = false) : stream_(stream)
     {
         for (int i = 0; i < helpers; ++i) th_.emplace_back([this] { loop(); });
     }
@@ -117,8 +119,12 @@ private:
                 off -= np * piece;
             }
             const size_t len = seg[s].bytes - off < piece ? seg[s].bytes - off : piece;
-            memcpy(static_cast<char*>(seg[s].dst) + off, static_cast<const char*>(seg[s].src) + off,
-                   len);
+            if (stream_)
+                stream_copy(static_cast<char*>(seg[s].dst) + off,
+                            static_cast<const char*>(seg[s].src) + off, len);
+            else
+                memcpy(static_cast<char*>(seg[s].dst) + off,
+                       static_cast<const char*>(seg[s].src) + off, len);
         }
     }
 
@@ -150,6 +156,7 @@ private:
     std::atomic<int> next_{0};
     unsigned gen_ = 0;
     bool open_ = false, stop_ = false;
+    const bool stream_;
 };
 
 }  // namespace youth

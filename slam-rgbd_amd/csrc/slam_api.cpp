@@ -25,6 +25,7 @@
 #include <cmath>
 #include <condition_variable>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <string>
@@ -126,6 +127,11 @@ struct youth_frame_queue {
     // the producer's copy (youth_queue_push): 1 streaming stores
     // (youth::stream_copy; YOUTH_SLAM_PUSH_COPY=nt), 0 memcpy (=memcpy)
     int copy_mode = 1;
+    // YOUTH_SLAM_PUSH_THREADS=k (k >= 1): a frame of >= 256 KB is copied by
+    // the producer and k helper threads (host_copy.h; one producer at a time,
+    // a concurrent producer copies alone); 0 (default): the producer alone
+    std::unique_ptr<youth::HostCopyPool> copier;
+    std::mutex copier_mu;
     size_t pinned_bytes = 0;  // page-locked bytes allocated and not freed
     int pinned_count = 0;     // page-locked buffers allocated and not freed
 };
@@ -296,6 +302,8 @@ youth_frame_queue* youth_queue_create(int high_water, int low_water)
     q->high = high_water;
     q->low = low_water;
     if (const char* e = getenv("YOUTH_SLAM_PUSH_COPY")) q->copy_mode = strcmp(e, "memcpy") == 0 ? 0 : 1;
+    if (const char* e = getenv("YOUTH_SLAM_PUSH_THREADS"))
+        if (atoi(e) > 0) q->copier.reset(new youth::HostCopyPool(std::min(atoi(e), 7), q->copy_mode == 1));
     return q;
 }
 
@@ -319,7 +327,18 @@ int youth_queue_push(youth_frame_queue* q, const int16_t* depth, int width, int 
     int kind = 0;
     trace(YOUTH_SLAM_EV_PUSH_BEGIN, youth_queue_size(q));
     if (!buf_get(q, n, it, &kind)) return YOUTH_ENOMEM;
-    if (q->copy_mode == 1)
+    bool copied = false;
+    if (q->copier && n * sizeof(int16_t) >= ((size_t)256 << 10)) {
+        std::unique_lock<std::mutex> lk(q->copier_mu, std::try_to_lock);
+        if (lk.owns_lock()) {
+            const youth::HostCopyPool::Seg seg{it.buf, depth, n * sizeof(int16_t)};
+            q->copier->run(&seg, 1, n * sizeof(int16_t) / (2 * (q->copier->helpers() + 1)));
+            copied = true;
+        }
+    }
+    if (copied)
+        ;
+    else if (q->copy_mode == 1)
         youth::stream_copy(it.buf, depth, n * sizeof(int16_t));
     else
         memcpy(it.buf, depth, n * sizeof(int16_t));

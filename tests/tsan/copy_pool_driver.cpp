@@ -13,9 +13,9 @@
 
 #include "host_copy.h"
 
-static int check_jobs(int helpers, int jobs, unsigned seed)
+static int check_jobs(int helpers, int jobs, unsigned seed, bool stream = false)
 {
-    youth::HostCopyPool pool(helpers);
+    youth::HostCopyPool pool(helpers, stream);
     std::mt19937 rng(seed);
     for (int j = 0; j < jobs; ++j) {
         const int n = 1 + (int)(rng() % 8);
@@ -43,6 +43,9 @@ int main()
 {
     int bad = 0;
     for (int h = 0; h <= 4; ++h) bad |= check_jobs(h, 60, 1234u + h);
+    // streaming stores (the SLAM producer's copy, youth::stream_copy): odd
+    // sizes and unaligned segments included
+    for (int h = 0; h <= 2; ++h) bad |= check_jobs(h, 40, 777u + h, true);
     // pools used concurrently from four threads (one caller per pool)
     std::vector<std::thread> th;
     std::vector<int> rc(4, 0);

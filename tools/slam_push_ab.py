@@ -2,7 +2,8 @@
 """processSlamFrame producer-copy A/B: the backlogged
 drop-in rate from one Python producer (bench.py's slam_api leg) and from the
 plain-C producer (slam_rate), YOUTH_SLAM_PUSH_COPY=memcpy vs nt (streaming
-stores), interleaved rounds on one box; each line: mode, rate, push us/frame."""
+stores), optionally with YOUTH_SLAM_PUSH_THREADS helpers (mode "nt+2"), interleaved
+rounds on one box; each line: mode, rate, push us/frame."""
 import json
 import os
 import subprocess
@@ -22,7 +23,9 @@ print(json.dumps({"value": r["value"], "push_us": float(np.median(r["push_us_per
 ''' % (ROOT, ROOT)
 for rnd in range(rounds):
     for m in modes:
-        env = dict(os.environ, YOUTH_SLAM_PUSH_COPY=m)
+        # a mode is <copy>[+<helper threads>], e.g. nt+2
+        cp, _, th = m.partition("+")
+        env = dict(os.environ, YOUTH_SLAM_PUSH_COPY=cp, YOUTH_SLAM_PUSH_THREADS=th or "0")
         r = subprocess.run([sys.executable, "-c", child], env=env, capture_output=True, text=True,
                            timeout=300, cwd=ROOT)
         if r.returncode:
