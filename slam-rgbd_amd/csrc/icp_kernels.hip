@@ -2042,7 +2042,15 @@ constexpr int kCoopPrepPair = kCoopPrepShards * kCoopShardStride;  // words per 
 constexpr int kCoopSetWords = kCoopPrepWords + kCoopMaxPairs * kCoopPrepPair;
 constexpr int kCoopTileH = 24;  // fused prep tiles: 64 x 24 pixels (one per workgroup of a 640x480 pair: 200 tiles, G = 200)
 constexpr int kCoopTileHTall = 80;  // 64 x 80 (= 10 px per lane x 512: one per workgroup of a 1280x960 pair, G = 240)
-constexpr unsigned kCoopSpinMax = 1u << 22;  // polls (~1 us each): seconds, never reached
+// Polls before a wait gives up (~0.5-1 us each: ~35-65 ms).  A wait of a
+// co-resident grid ends within microseconds; one that reaches the bound has
+// a workgroup that never started (the grid is not co-resident: another
+// process holds CUs), and the tracker's realign then runs after one stalled
+// frame instead of a stall of seconds (round 6; 2^22 polls, ~4 s, before).
+// The bound counts polls, not time: a wave that is preempted does not poll.
+// (A bound chosen per iteration, short for iteration 0 only, cost C2 1.9 %:
+// profiles/r06/coop_spin_bound_ab_r6j.txt.)
+constexpr unsigned kCoopSpinMax = 1u << 16;
 constexpr int kCoopMaxChain = YOUTH_TRACK_MAX_BATCH;  // frames per tracker micro-batch
 
 struct CoopState {
@@ -2086,7 +2094,8 @@ struct CoopState {
     int part_cap, part_reset;
     int poll_delay;  // x 64 clocks before the first pass over the rows
     unsigned spin_max;  // polls before a wait gives up (kCoopSpinMax; the test hook's less)
-    int stall_chunk;    // test hook: this chunk of pair 0 never stores iteration 1's row (-1: none)
+    int stall_chunk;    // test hook: this chunk of pair 0 never stores iteration stall_iter's row (-1: none)
+    int stall_iter;
 };
 
 // Phase timestamps for tools/coopbench only (never in the product build):
@@ -2451,7 +2460,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_icp_coop(const int16_t* __restr
             // value of iteration k is (see the hand-off above)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             double sum = 0.0;
-            if (lane < kPartStride && !(k == 1 && p == 0 && c == cs.stall_chunk)) {
+            if (lane < kPartStride && !(k == cs.stall_iter && p == 0 && c == cs.stall_chunk)) {
                 if (lane < kNeq) {  // the waves' sums as a pairwise tree (3 dependent adds)
                     double r[kThreads / 64];
 #pragma unroll
@@ -2692,6 +2701,7 @@ struct youth_icp_ctx {
     int coop_poll_delay = -1;        // YOUTH_ICP_COOP_POLL_DELAY (x 64 clocks); -1: G / 8
     int coop_stall_once = -1;        // YOUTH_ICP_TEST_COOP_STALL (test hook): chunk that stalls
     int coop_stall_left = 0;         // coop launches the hook still stalls
+    int coop_stall_iter = 1;         // YOUTH_ICP_TEST_COOP_STALL_ITER: the iteration whose row is lost
     bool realign_stall = false;      // YOUTH_ICP_TEST_REALIGN_STALL=1 (test hook): realigns' coop launches stall
     int last_coop_G = 0, last_coop_px = 0;
     bool last_coop = false;          // the last align ran k_icp_coop
@@ -3179,7 +3189,10 @@ static int launch_coop(youth_icp_ctx* c, hipStream_t s, const int16_t* dsrc, Pai
     // context's first coop launches lose one row, so their waits time out
     // after ~20 ms
     cs.stall_chunk = c->coop_stall_once;
-    cs.spin_max = c->coop_stall_once >= 0 ? 20000u : kCoopSpinMax;
+    cs.stall_iter = c->coop_stall_iter;
+    // a lost iteration-0 row is ended by the product's bound itself (the
+    // test of it); a later one by the hook's shorter bound
+    cs.spin_max = c->coop_stall_once >= 0 && c->coop_stall_iter != 0 ? 20000u : kCoopSpinMax;
     if (c->coop_stall_once >= 0 && --c->coop_stall_left <= 0) c->coop_stall_once = -1;
     const float4* recs = c->d_rec;
     size_t P = c->P;
@@ -3677,6 +3690,8 @@ youth_icp_ctx* youth_icp_create(int device, int W, int H, int max_frames,
                             "cooperative launch(es) of this context time out\n",
                     cst, c->coop_stall_left);
         }
+        const char* sit = getenv("YOUTH_ICP_TEST_COOP_STALL_ITER");
+        if (sit && atoi(sit) >= 0) c->coop_stall_iter = atoi(sit);
         const char* rst = getenv("YOUTH_ICP_TEST_REALIGN_STALL");
         c->realign_stall = rst && *rst && *rst != '0';
         if (c->realign_stall)

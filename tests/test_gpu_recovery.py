@@ -178,3 +178,30 @@ def test_slam_backlog_timeout_persistent_fallback(monkeypatch):
     err = max(_pose_err(a, b) for a, b in zip(got["T"], base["T"]))
     assert err <= 1e-12, err
     assert np.array_equal(got["st"], base["st"])
+
+
+def test_entry_wait_gives_up_fast_and_tracker_recovers(monkeypatch):
+    """A grid whose entry barrier never completes (hook: chunk 7's
+    iteration-0 row is lost, with the product's own spin bound, not the
+    hook's shorter one) is what a grid that is not co-resident looks like:
+    its waits give up after kCoopSpinMax polls (~35-65 ms; ~4 s before round
+    6), the frame comes back TIMEOUT, and the realign gives the undisturbed
+    pose."""
+    import time
+    frames, _ = youth_synth.sequence(1, 3)
+    with youth_icp.IcpContext(640, 480, 2) as ctx:
+        want = [ctx.track_frame(f)[:2] for f in frames][1:]
+    monkeypatch.setenv("YOUTH_ICP_TEST_COOP_STALL", "7")
+    monkeypatch.setenv("YOUTH_ICP_TEST_COOP_STALL_ITER", "0")
+    with youth_icp.IcpContext(640, 480, 2) as ctx:
+        assert not ctx.track_frame(frames[0])[2]
+        t0 = time.perf_counter()
+        T1, st1, has = ctx.track_frame(frames[1])
+        dt = time.perf_counter() - t0
+        assert has and st1 & youth_icp.STATUS_TIMEOUT, st1
+        assert dt < 1.5, dt                        # the bound, not round 5's ~4 s
+        T, st = ctx.track_realign(frames[0], frames[1])
+        assert np.array_equal(T, want[0][0]) and st == want[0][1]
+        T2, st2, _ = ctx.track_frame(frames[2])    # the tracker carries on
+        assert np.array_equal(T2, want[1][0]) and st2 == want[1][1]
+        print(f"\nspin-bound timeout after {dt * 1e3:.1f} ms")
