@@ -212,7 +212,10 @@ int youth_icp_set_concurrency(youth_icp_ctx* ctx, int contexts);
  * cached context; batches of >= 32 pairs are pipelined in 16-pair chunks
  * (H2D of chunk k overlaps the align of chunk k-1).  Returns YOUTH_OK even
  * when a pair's solve was skipped: per-pair status (YOUTH_STATUS_*) is
- * reported by youth_icp_align_batch_multi's status_out. */
+ * reported by youth_icp_align_batch_multi's status_out.  A chunk whose
+ * cooperative launch timed out (a GPU shared with another process: the grid
+ * was not co-resident) is aligned again on the persistent kernel before the
+ * call returns, so neither call hands out a TIMEOUT pose (stderr says so). */
 int youth_icp_align_batch(const int16_t* src, const int16_t* dst, int n_pairs,
                           int W, int H, const youth_intrinsics* K, int iters,
                           float* T_out, int32_t* assoc_out);

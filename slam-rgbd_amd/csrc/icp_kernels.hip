@@ -2717,6 +2717,7 @@ struct youth_icp_ctx {
     long long trk_chained = 0;        // micro-batch launches so far (youth_icp_track_chained)
     long long trk_chained_frames = 0; // frames those launches aligned (youth_icp_track_chained_frames)
     long long trk_realigned[3] = {};  // youth_icp_track_realign: coop / persistent / still failed
+    long long batch_realigned = 0;    // host batch API chunks realigned after a coop timeout
     int queues = 0;                  // k_icp work queues (YOUTH_ICP_QUEUES=1..8; 0: by batch size)
     int share = 1;                   // contexts launching k_icp concurrently (set_concurrency)
     int prep_xcd_map = 0;             // YOUTH_ICP_PREP_XCD_MAP=1: k_prep tiles contiguous per XCD (slower)
@@ -4105,7 +4106,8 @@ static int batch_on_device(int dev, const int16_t* src, const int16_t* dst, int 
     if (rc) return rc;
     hipStream_t s = c->stream;
     if (!c->xfer) HIP_TRY(hipStreamCreateWithFlags(&c->xfer, hipStreamNonBlocking));
-    if (status_out && !c->d_status_out)
+    // per-pair status on every call: a timed-out cooperative chunk is realigned below
+    if (!c->d_status_out)
         HIP_TRY(hipMalloc(&c->d_status_out, (size_t)c->max_frames * sizeof(int32_t)));
     auto drain = [c, s](int code) {
         (void)hipStreamSynchronize(c->xfer);
@@ -4148,7 +4150,42 @@ static int batch_on_device(int dev, const int16_t* src, const int16_t* dst, int 
             first_lanes = c->lanes;
         else
             mixed |= memcmp(&first_lanes, &c->lanes, sizeof(youth_lanes)) != 0;
-        if (status_out) {
+        hipLaunchKernelGGL(k_status_out, dim3((cnt + 255) / 256), dim3(256), 0, s,
+                           c->d_status, cnt, (const unsigned*)(c->d_head + kQError),
+                           c->d_status_out + p0);
+        if ((e = hipGetLastError()) != hipSuccess)
+            return drain(set_error(YOUTH_EHIP, "align_batch: %s", hipGetErrorString(e)));
+    }
+    // A chunk of <= 16 pairs is one cooperative launch sized to an idle
+    // device; on a GPU shared with other processes its grid may not be
+    // co-resident, and it then times out (kCoopSpinMax polls, ~50 ms) with
+    // partly iterated poses.  Such a chunk is aligned again, synchronously, on
+    // the persistent k_prep + k_icp, which waits only on running workgroups:
+    // the same poses up to fp64 summation order (its depth frames are still
+    // on the device).  The caller never receives a TIMEOUT pose from here.
+    {
+        std::vector<int32_t> st((size_t)n_pairs);
+        hipError_t e = hipMemcpyAsync(st.data(), c->d_status_out, (size_t)n_pairs * sizeof(int32_t),
+                                      hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return drain(set_error(YOUTH_EHIP, "align_batch: %s", hipGetErrorString(e)));
+        for (int k = 0; k < n_chunks; ++k) {
+            const size_t p0 = (size_t)k * chunk;
+            const int cnt = (int)std::min<size_t>(chunk, n_pairs - p0);
+            bool to = false;
+            for (int i = 0; i < cnt; ++i) to |= (st[p0 + i] & YOUTH_STATUS_TIMEOUT) != 0;
+            if (!to) continue;
+            fprintf(stderr, "youth_icp: align_batch: a cooperative launch of %d pair(s) timed out "
+                            "(GPU shared with another process?); realigned on the persistent kernel\n",
+                    cnt);
+            const bool coop_was = c->coop;
+            c->coop = false;
+            rc = youth_icp_align_pairs_device(c, d_s + p0 * N, d_d + p0 * N, cnt, nullptr,
+                                              c->d_Tout + p0 * 16, s);
+            c->coop = coop_was;
+            if (rc) return drain(rc);
+            ++c->batch_realigned;
+            mixed = true;  // this chunk's lane partition is the persistent kernel's
             hipLaunchKernelGGL(k_status_out, dim3((cnt + 255) / 256), dim3(256), 0, s,
                                c->d_status, cnt, (const unsigned*)(c->d_head + kQError),
                                c->d_status_out + p0);

@@ -570,7 +570,9 @@ void worker_main(int device)
         trace(YOUTH_SLAM_EV_COLLECT_BEGIN, (int)pend.size() + 1);
         int st = youth_icp_track_collect(ctx, T_rel, &has_ref);
         trace(YOUTH_SLAM_EV_COLLECT_END, pr0.last ? 1 : 0);
-        if (st >= 0 && has_ref && (st & YOUTH_STATUS_TIMEOUT)) {
+        // (a frame of a sequence that a reset ended is not recorded: no retry)
+        const bool keep = record && !g_reset.load();
+        if (st >= 0 && has_ref && (st & YOUTH_STATUS_TIMEOUT) && keep) {
             // never composed: aligned again from the two frames' host buffers
             // (the cooperative plan, bit-identical when it completes; else the
             // persistent kernel); still timed out = lost
@@ -598,6 +600,7 @@ void worker_main(int device)
         }
         ref_hold = pr0.item;
         ref_valid = true;
+        if (!keep) return;
         if (st & YOUTH_STATUS_TIMEOUT) {
             // no pose for this frame: it is left out of the trajectory and the
             // next frame composes onto the last recorded pose (no motion
@@ -605,7 +608,6 @@ void worker_main(int device)
             fprintf(stderr, "youth_icp: frame %u lost (align timed out twice)\n", pr0.ts);
             return;
         }
-        if (!record || g_reset.load()) return;
         std::lock_guard<std::mutex> lk(g_slam_mu);
         // resetSlam raises g_reset under this lock before it clears the
         // trajectory: a frame of the old sequence that passed the check

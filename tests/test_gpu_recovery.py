@@ -205,3 +205,30 @@ def test_entry_wait_gives_up_fast_and_tracker_recovers(monkeypatch):
         T2, st2, _ = ctx.track_frame(frames[2])    # the tracker carries on
         assert np.array_equal(T2, want[1][0]) and st2 == want[1][1]
         print(f"\nspin-bound timeout after {dt * 1e3:.1f} ms")
+
+
+def test_host_batch_api_realigns_a_timed_out_chunk(monkeypatch, capfd):
+    """The host batch API (youth_icp_align_batch / _multi) never hands out a
+    TIMEOUT pose: a chunk whose cooperative launch timed out is aligned again
+    on the persistent kernel from the frames still on the device.  The cached
+    batch context is recreated under the stall hook (intrinsics switched away
+    and back); the poses equal an undisturbed call's within fp32 rounding,
+    every status is 0, every pose is within 1e-5 of the oracle, and the retry
+    is reported on stderr."""
+    src, dst, _ = youth_synth.pairs(71, 4)
+    Kb = youth_icp.Intrinsics(571.25, 571.25, 320.0, 240.0, 1000.0)
+    Ka = youth_icp.Intrinsics(571.5, 571.5, 320.0, 240.0, 1000.0)
+    want = youth_icp.align_batch(src, dst, K=Kb, iters=10)[0]
+    youth_icp.align_batch(src[:1], dst[:1], K=Ka, iters=10)     # the cached context moves to Ka
+    monkeypatch.setenv("YOUTH_ICP_TEST_COOP_STALL", "7")
+    capfd.readouterr()
+    got, st = youth_icp.align_batch_multi(src, dst, K=Kb, iters=10, devices=[0])   # recreated: hook on
+    err = capfd.readouterr().err
+    monkeypatch.delenv("YOUTH_ICP_TEST_COOP_STALL")
+    assert "realigned on the persistent kernel" in err, err[-2000:]
+    assert not np.asarray(st).any(), st
+    assert float(np.abs(np.asarray(got) - np.asarray(want)).max()) <= 1e-6
+    Ko = [Kb.fx, Kb.fy, Kb.cx, Kb.cy, Kb.depth_scale]
+    for i in range(src.shape[0]):
+        To = oracle.align(src[i], dst[i], K=Ko)[0]
+        assert _pose_err(np.asarray(got[i], np.float64), To) <= POSE_TOL
