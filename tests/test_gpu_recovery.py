@@ -232,3 +232,28 @@ def test_host_batch_api_realigns_a_timed_out_chunk(monkeypatch, capfd):
     for i in range(src.shape[0]):
         To = oracle.align(src[i], dst[i], K=Ko)[0]
         assert _pose_err(np.asarray(got[i], np.float64), To) <= POSE_TOL
+
+
+def test_slam_few_matches_frames_are_composed_with_their_status():
+    """YOUTH_STATUS_FEW_MATCHES (youth_icp.h): a frame with no valid depth
+    skips every update, so its relative pose is the identity ("no motion"),
+    which is composed; the status bits are kept with the pose and counted.
+    The frame after it (aligned against the empty frame) likewise."""
+    frames, _ = youth_synth.sequence(0, 4)
+    seq = np.stack([frames[0], np.zeros_like(frames[0]), frames[2], frames[3]])
+    youth_icp.initSlamModule(CFG, "ORBvoc.txt")
+    try:
+        for k in range(seq.shape[0]):
+            assert youth_icp.processSlamFrame(seq[k], None, 640, 480, 10 + k) == 1
+            assert youth_icp.slam_wait_idle(20000) == 1
+        ts, T = youth_icp.slam_trajectory()
+        st, few, deg = youth_icp.slam_status()
+        re = youth_icp.slam_realigned()
+    finally:
+        youth_icp.stopSlamModule()
+    assert list(ts) == [10, 11, 12, 13]
+    assert list(st) == [0, youth_icp.STATUS_FEW_MATCHES, youth_icp.STATUS_FEW_MATCHES, 0], st
+    assert few == 2 and deg == 0 and re == {"coop": 0, "persistent": 0, "lost": 0}
+    assert np.array_equal(T[1], np.eye(4)) and np.array_equal(T[2], np.eye(4))
+    T3 = oracle.align(seq[3], seq[2])[0]
+    assert _pose_err(T[3], T3) <= POSE_TOL
