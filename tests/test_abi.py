@@ -5,6 +5,7 @@ No compute calls here."""
 import ctypes
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -230,3 +231,64 @@ def test_host_wrappers_reject_mismatched_shapes():
         youth_icp.align_batch_multi(a, np.zeros((3, 8, 8), np.int16))
     with pytest.raises(ValueError):
         youth_icp.align_batch(np.zeros(64, np.int16), np.zeros(64, np.int16))
+
+
+_NULL_SWEEP = r"""
+import ctypes, re, sys
+text = open(sys.argv[1]).read()
+text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+text = re.sub(r"typedef[^;]*;", "", text)
+lib = ctypes.CDLL(sys.argv[2])
+for ret, name, args in re.findall(r"\n\s*([A-Za-z_][\w ]*?\**)\s*\b(youth_\w+)\(([^;{]*)\)\s*;", text):
+    ret = ret.strip()
+    args = " ".join(args.split())
+    if not (args.startswith(("youth_icp_ctx*", "const youth_icp_ctx*", "youth_frame_queue*"))
+            or name.startswith("youth_slam_")):
+        continue
+    n = 0 if args in ("", "void") else args.count(",") + 1
+    f = getattr(lib, name)
+    f.restype = (None if ret == "void" else ctypes.c_longlong if ret.startswith("long long")
+                 else ctypes.c_void_p if ret.endswith("*") else ctypes.c_int)
+    f.argtypes = [ctypes.c_void_p] * n
+    print(name, ret, f(*([None] * n)), flush=True)
+"""
+
+
+def test_null_arguments_are_refused_not_dereferenced(tmp_path):
+    """Every entry point that takes a context or a queue, and every
+    youth_slam_* query, called with NULL / zero for all of its arguments (no
+    module running): it returns an error or an empty answer, and nothing
+    dereferences the NULL.  Calls run in a child process, so a crash fails the
+    test instead of the test runner."""
+    script = tmp_path / "sweep.py"
+    script.write_text(_NULL_SWEEP)
+    r = subprocess.run([sys.executable, str(script), os.path.join(ROOT, "include", "youth_icp.h"),
+                        HEADERS["youth_icp.h"]], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    res = {}
+    for line in r.stdout.splitlines():
+        name, *_, val = line.split()
+        res[name] = val
+    assert len(res) >= 45, sorted(res)
+    einval = str(youth_icp.YOUTH_EINVAL)
+    must_fail = [n for n in res if n.startswith(("youth_icp_align", "youth_icp_track_submit",
+                                                  "youth_icp_track_collect", "youth_icp_track_frame",
+                                                  "youth_icp_track_realign", "youth_icp_get_",
+                                                  "youth_icp_set_", "youth_icp_sync",
+                                                  "youth_icp_track_host", "youth_queue_p"))
+                 and n != "youth_icp_track_realigned"]
+    assert len(must_fail) >= 20
+    assert all(res[n] == einval for n in must_fail), {n: res[n] for n in must_fail}
+    # counters and sizes of nothing are 0; void calls return
+    for n in ("youth_icp_track_pending", "youth_icp_track_chained", "youth_icp_track_realigned",
+              "youth_queue_size", "youth_slam_trajectory_length", "youth_slam_get_trajectory",
+              "youth_slam_realigned", "youth_slam_queue_size"):
+        assert res[n] == "0", (n, res[n])
+    assert res["youth_icp_destroy"] == "None" and res["youth_slam_wait_stopped"] == "None"
+    # the reference API with NULL buffers (SLAM.h: 0 = failure)
+    lib = ctypes.CDLL(HEADERS["youth_icp.h"])
+    lib.processSlamFrame.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_uint32]
+    assert lib.processSlamFrame(None, None, 640, 480, 0) == 0
+    lib.saveSlamMap.argtypes = [ctypes.c_char_p]
+    assert lib.saveSlamMap(None) == 0
