@@ -937,6 +937,34 @@ def test_max_frame_size_8192x8192():
     assert np.array_equal(assoc[0], idx)
 
 
+@pytest.mark.parametrize("W,H", [(16384, 48), (48, 16384)])
+def test_extreme_aspect_frames(W, H):
+    """The widest and the tallest frames youth_icp_create accepts with a
+    short other side (W or H = 16384): 256 tiles across one row (or down one
+    column), the 24-bit index multiply at its largest row stride, and partial
+    tiles on the short side.  Two pairs in one batch and one pair per call
+    (the cooperative kernel when its plan fits): poses within 1e-5 of the
+    oracle, association at the final pose bit-exact."""
+    import torch
+    K = youth_icp.default_intrinsics(W, H)
+    src, dst, _ = youth_synth.pairs(3, 2, W, H)
+    Tg, assoc = youth_icp.align_batch(src, dst, K=K, want_assoc=True)
+    for p in range(2):
+        To, _, st, _ = oracle.align(src[p], dst[p], K)
+        assert st == 0 and _pose_err(Tg[p], To) <= POSE_TOL, p
+        idx = oracle.associate(src[p], dst[p], Tg[p][:3], K)
+        assert int((idx >= 0).sum()) > W * H // 8
+        assert np.array_equal(assoc[p], idx), p
+    ctx = youth_icp.IcpContext(W, H, 2, K=K)
+    ds, dd = torch.from_numpy(src[:1]).cuda(), torch.from_numpy(dst[:1]).cuda()
+    ctx.align_pairs_device(ds.data_ptr(), dd.data_ptr(), 1)
+    T64, _, st = ctx.get_poses(1)
+    plan = ctx.get_plan()
+    ctx.close()
+    To, _, sto, _ = oracle.align(src[0], dst[0], K)
+    assert st[0] == sto == 0 and _pose_err(T64[0], To) <= POSE_TOL, plan
+
+
 def test_plain_c_batch_multi_demo(tmp_path):
     """youth_icp_align_batch_multi driven from plain C99 over every visible
     device (examples/batch_multi_demo.c): every pose within 1e-5 of the
